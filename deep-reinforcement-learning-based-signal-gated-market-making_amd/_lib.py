@@ -1,0 +1,138 @@
+"""ctypes binding of libsgmm.so (the C ABI declared in include/sgmm.h).
+
+The library is the product's only compute path.  If it is missing or cannot
+load, every GPU entry point raises -- there is deliberately no CPU fallback.
+
+torch is imported first so that libsgmm.so's libamdhip64.so.7 dependency
+resolves to the HIP runtime torch already loaded (one runtime per process;
+torch tensors' device pointers and streams are then valid in our calls).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede loading libsgmm.so, see module doc)
+
+PKG_DIR = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("SGMM_LIB", PKG_DIR / "libsgmm.so"))
+ABI_VERSION = 1
+
+
+class SgmmError(RuntimeError):
+    pass
+
+
+# ----------------------------------------------------------------- structs (mirror include/sgmm.h)
+class EnvParams(ctypes.Structure):
+    _fields_ = [("phi", ctypes.c_double), ("tick", ctypes.c_double), ("fee", ctypes.c_double),
+                ("idle_penalty", ctypes.c_double), ("i_max", ctypes.c_int32),
+                ("i_min", ctypes.c_int32), ("act_scale", ctypes.c_float),
+                ("adv_scale", ctypes.c_float)]
+
+
+class Ticks(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in
+                ("s1n", "s2n", "mid_next", "best_ask", "best_bid", "buy_max", "sell_min")]
+
+
+class Episodes(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("max_len", ctypes.c_int32),
+                ("total_steps", ctypes.c_int64), ("inv_min", ctypes.c_int32),
+                ("inv_max", ctypes.c_int32), ("genome", ctypes.c_void_p),
+                ("adv", ctypes.c_void_p), ("tick_off", ctypes.c_void_p),
+                ("len", ctypes.c_void_p), ("step_off", ctypes.c_void_p),
+                ("param", ctypes.c_void_p)]
+
+
+class GAState(ctypes.Structure):
+    _fields_ = [("sigma_mm", ctypes.c_double), ("sigma_adv", ctypes.c_double),
+                ("best_val", ctypes.c_double), ("last_train_f", ctypes.c_double),
+                ("last_val_f", ctypes.c_double), ("no_improve", ctypes.c_int32),
+                ("best_idx", ctypes.c_int32), ("adv_best_idx", ctypes.c_int32),
+                ("gen", ctypes.c_int32), ("improved", ctypes.c_int32),
+                ("decayed", ctypes.c_int32), ("patience", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("decay", ctypes.c_double)]
+
+
+class GAHistory(ctypes.Structure):
+    _fields_ = [("train_f", ctypes.c_double), ("val_f", ctypes.c_double),
+                ("sigma_after", ctypes.c_double), ("train_trades", ctypes.c_int32),
+                ("val_trades", ctypes.c_int32), ("best_idx", ctypes.c_int32),
+                ("flags", ctypes.c_int32)]
+
+
+assert ctypes.sizeof(EnvParams) == 48
+assert ctypes.sizeof(GAState) == 80
+assert ctypes.sizeof(GAHistory) == 40
+
+_VP, _I32, _I64, _U32, _U64, _D, _SZ = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
+                                        ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
+                                        ctypes.c_size_t)
+
+# name -> (restype, argtypes); the symbol set of include/sgmm.h
+SIGNATURES = {
+    "sgmm_abi_version": (ctypes.c_int, []),
+    "sgmm_last_error": (ctypes.c_char_p, []),
+    "sgmm_env_step_batch": (ctypes.c_int, [_VP] * 17 + [_I64, _VP]),
+    "sgmm_policy_forward": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _I64, _VP]),
+    "sgmm_adversary_forward": (ctypes.c_int, [_VP, _I64, _VP, _VP, _VP, _I64, _VP]),
+    "sgmm_rollout_workspace_size": (_SZ, [_I32, _I64, _I32]),
+    "sgmm_rollout_fitness": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                            _VP, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _SZ, _VP]),
+    "sgmm_rollout_trace": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                          _VP, _I64, _I32, _VP, _I64] + [_VP] * 16),
+    "sgmm_ga_ask": (ctypes.c_int, [_VP, _I64, _VP, _U64, _U32, _U32, _I32, _I32, _VP, _I64, _VP]),
+    "sgmm_ga_state_init": (ctypes.c_int, [_VP, _D, _I32, _D, _VP]),
+    "sgmm_ga_tell": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _VP, _I64, _I64,
+                                    _I64, _U64, _U32, _VP, _VP]),
+    "sgmm_ga_val_update": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _VP]),
+}
+
+_lib = None
+
+
+def load(path: Path | None = None):
+    """Load libsgmm.so and bind every symbol; raise SgmmError if impossible."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise SgmmError(f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                        f"g.build()'` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    L = ctypes.CDLL(str(p))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.sgmm_abi_version() != ABI_VERSION:
+        raise SgmmError(f"libsgmm ABI {L.sgmm_abi_version()} != {ABI_VERSION}")
+    if path is None:
+        _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = _lib.sgmm_last_error().decode() if _lib is not None else ""
+        raise SgmmError(f"{what} failed (rc={rc}): {msg}")
+
+
+def ptr(t):
+    """Raw device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_gpu():
+    if not torch.cuda.is_available():
+        raise SgmmError("no HIP device visible: the sgmm rollout path runs only on the GPU "
+                        "(MI355X / gfx950); there is no CPU fallback")

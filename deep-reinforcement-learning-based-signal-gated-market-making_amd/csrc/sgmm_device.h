@@ -1,0 +1,197 @@
+// sgmm_device.h -- device-side building blocks shared by the gfx950 kernels.
+//
+// Everything here is written for CDNA4 (wave64, gfx950) directly.  The
+// numerics contract (see include/sgmm.h) is implemented once, here:
+//   * ftp_fill / ftp_step: FTPEnv.step (Env/market_env.py:22-67) in float64,
+//     reference operation order; the library is compiled with
+//     -ffp-contract=off so `a + b * c` never becomes v_fma_f64.
+//   * mlp_*: TradingPolicy / AdversaryPolicy forward (models/model.py:5-57),
+//     every dot product the k-ordered fused chain from the bias (v_fma_f32).
+//   * philox / normal4: counter-based N(0,1) stream for NeuroEvolution.ask.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sgmm.h"
+
+namespace sgmm {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float relu(float a) { return a < 0.0f ? 0.0f : a; }
+
+// float -> int action: saturating, NaN -> INT32_MIN (the x86 cvtt value numpy's
+// astype(int) produces).  Values are already integral (rint) when called.
+__device__ __forceinline__ int32_t act_to_int(float r) {
+    if (r != r) return INT32_MIN;
+    if (r >= 2147483520.0f) return INT32_MAX;
+    if (r <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)r;
+}
+
+// ---------------------------------------------------------------- FTPEnv.step
+struct StepOut {
+    double reward, pnl, fee_paid;
+    int32_t inv;
+    int fill_buy, fill_sell;
+    double cash_delta_buy, cash_delta_sell;  // applied to cash in reference order
+};
+
+// One FTPEnv.step from inventory `inv` with final offsets (adversary already
+// added, market_env.py:25-28).  Pure function of its inputs.
+__device__ __forceinline__ StepOut ftp_step(const sgmm_env_params& p, int32_t inv,
+                                            int32_t off_a, int32_t off_b, double mid_next,
+                                            double best_ask, double best_bid, double buy_max,
+                                            double sell_min) {
+    StepOut o;
+    const double qa = best_ask + (double)off_a * p.tick;   // market_env.py:30
+    const double qb = best_bid - (double)off_b * p.tick;   // market_env.py:31
+    o.fill_buy = (inv < p.i_max) && (qb >= sell_min);      // :34,:37 (NaN -> no fill)
+    o.fill_sell = (inv > p.i_min) && (qa <= buy_max);      // :35,:38
+    double pnl = 0.0, fees = 0.0;
+    int32_t q = inv;
+    o.cash_delta_buy = 0.0;
+    o.cash_delta_sell = 0.0;
+    if (o.fill_buy) {                                      // :44-49
+        const double f = qb * p.fee;
+        q += 1;
+        o.cash_delta_buy = qb + f;
+        pnl += (mid_next - qb) - f;
+        fees += f;
+    }
+    if (o.fill_sell) {                                     // :50-55
+        const double f = qa * p.fee;
+        q -= 1;
+        o.cash_delta_sell = qa - f;
+        pnl += (qa - mid_next) - f;
+        fees += f;
+    }
+    o.inv = q;
+    o.pnl = pnl;
+    o.fee_paid = fees;
+    o.reward = pnl - p.phi * (double)(q < 0 ? -q : q);     // :57-58
+    return o;
+}
+
+// cash update with the reference's two separate in-place ops (:47, :53)
+__device__ __forceinline__ double apply_cash(double cash, const StepOut& o) {
+    if (o.fill_buy) cash -= o.cash_delta_buy;
+    if (o.fill_sell) cash += o.cash_delta_sell;
+    return cash;
+}
+
+// ---------------------------------------------------------------- policy MLP
+// Genome layout (parameters() order, model.py:8-15): W1[H,3] b1[H] W2[H,H]
+// b2[H] W3[2,H] b3[2].
+template <int H>
+struct GenomeLayout {
+    static constexpr int W1 = 0, B1 = 3 * H, W2 = 4 * H, B2 = 4 * H + H * H;
+    static constexpr int W3 = 5 * H + H * H, B3 = 7 * H + H * H, N = 7 * H + H * H + 2;
+};
+
+// Full forward for one state; `g` may be a per-lane or a uniform pointer.
+template <int H>
+__device__ __forceinline__ void mlp_forward(const float* __restrict__ g, float x0, float x1,
+                                            float x2, float& out0, float& out1) {
+    using L = GenomeLayout<H>;
+    float h1[H];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        float a = g[L::B1 + j];
+        a = __builtin_fmaf(g[L::W1 + 3 * j + 0], x0, a);
+        a = __builtin_fmaf(g[L::W1 + 3 * j + 1], x1, a);
+        a = __builtin_fmaf(g[L::W1 + 3 * j + 2], x2, a);
+        h1[j] = relu(a);
+    }
+    float o0 = g[L::B3 + 0], o1 = g[L::B3 + 1];
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        float a = g[L::B2 + j];
+#pragma unroll
+        for (int k = 0; k < H; ++k) a = __builtin_fmaf(g[L::W2 + j * H + k], h1[k], a);
+        const float h2 = relu(a);
+        // layer 3 accumulates in j order: the same chain as
+        // out_o = b3[o]; for j: out_o = fma(W3[o,j], h2[j], out_o)
+        o0 = __builtin_fmaf(g[L::W3 + j], h2, o0);
+        o1 = __builtin_fmaf(g[L::W3 + H + j], h2, o1);
+    }
+    out0 = o0;
+    out1 = o1;
+}
+
+// AdversaryPolicy (model.py:38-57): 3 -> 12 (ReLU) -> 2 (tanh), weights = the
+// first 74 floats of the genome row.
+__device__ __forceinline__ void adv_forward(const float* __restrict__ g, float x0, float x1,
+                                            float x2, float& out0, float& out1) {
+    float h[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        float a = g[36 + j];
+        a = __builtin_fmaf(g[3 * j + 0], x0, a);
+        a = __builtin_fmaf(g[3 * j + 1], x1, a);
+        a = __builtin_fmaf(g[3 * j + 2], x2, a);
+        h[j] = relu(a);
+    }
+    float o0 = g[72], o1 = g[73];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+        o0 = __builtin_fmaf(g[48 + j], h[j], o0);
+        o1 = __builtin_fmaf(g[60 + j], h[j], o1);
+    }
+    out0 = tanhf(o0);
+    out1 = tanhf(o1);
+}
+
+// Adversary delta for state (inventory, sell flag, buy flag): drl_engine.py:43-48
+// (round(tanh * scale)) and market_env.py:26 (round again: idempotent).
+__device__ __forceinline__ void adv_delta(const float* __restrict__ g, const sgmm_env_params& p,
+                                          int32_t inv, int fill_sell_prev, int fill_buy_prev,
+                                          int32_t& da, int32_t& db) {
+    float r0, r1;
+    adv_forward(g, (float)((double)inv / 2.0), fill_sell_prev ? 1.0f : 0.0f,
+                fill_buy_prev ? 1.0f : 0.0f, r0, r1);
+    da = act_to_int(rintf(r0 * p.adv_scale));
+    db = act_to_int(rintf(r1 * p.adv_scale));
+}
+
+// ---------------------------------------------------------------- Philox4x32-10
+struct U4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ U4 philox4x32_10(U4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+        const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Four N(0,1) floats for counter (block, individual, gen, stream) via
+// Box-Muller on two uniform pairs in (0,1].
+__device__ __forceinline__ void normal4(uint64_t seed, uint32_t stream_id, uint32_t gen,
+                                        uint32_t indiv, uint32_t block, float z[4]) {
+    const U4 r = philox4x32_10(U4{block, indiv, gen, stream_id}, (uint32_t)seed,
+                               (uint32_t)(seed >> 32));
+    const float inv32 = 2.3283064365386963e-10f;  // 2^-32
+    const float u0 = ((float)r.x + 1.0f) * inv32;  // (0, 1]
+    const float u1 = (float)r.y * inv32;           // [0, 1)
+    const float u2 = ((float)r.z + 1.0f) * inv32;
+    const float u3 = (float)r.w * inv32;
+    const float m0 = sqrtf(-2.0f * logf(u0 > 1.0f ? 1.0f : u0));
+    const float m1 = sqrtf(-2.0f * logf(u2 > 1.0f ? 1.0f : u2));
+    float s0, c0, s1, c1;
+    sincospif(2.0f * u1, &s0, &c0);
+    sincospif(2.0f * u3, &s1, &c1);
+    z[0] = m0 * c0;
+    z[1] = m0 * s0;
+    z[2] = m1 * c1;
+    z[3] = m1 * s1;
+}
+
+}  // namespace sgmm

@@ -1,0 +1,250 @@
+// sgmm_ga.hip -- the neuroevolution loop's bookkeeping on device, so a whole
+// generation (ask -> rollout -> tell -> validation update) is enqueued
+// without a host round trip.
+//
+// Reference: NeuroEvolution.ask/tell (models/model.py:59-76) and the
+// generation body of DRLEngine.train (Env/drl_engine.py:92-171).
+#include <cmath>
+
+#include "sgmm_device.h"
+#include "sgmm_internal.h"
+
+namespace sgmm {
+
+// ask: one thread per 4 consecutive parameters of one individual.
+// out = master + (z * (float)sigma): the reference's randn_like * sigma in
+// float32, then the float32 add (model.py:69-70).
+__device__ __forceinline__ void ask_row4(const float* __restrict__ master, int64_t n_params,
+                                         float sig, uint64_t seed, uint32_t sid, uint32_t gen,
+                                         uint32_t indiv, int64_t k4, float* dst) {
+    float z[4];
+    normal4(seed, sid, gen, indiv, (uint32_t)k4, z);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t k = 4 * k4 + q;
+        if (k < n_params) {
+            const float noise = z[q] * sig;
+            dst[q] = master[k] + noise;
+        }
+    }
+}
+
+__global__ void k_ga_ask(const float* __restrict__ master, int64_t n_params,
+                         const double* __restrict__ sigma, uint64_t seed, uint32_t sid,
+                         uint32_t gen, int32_t i0, int32_t n, float* __restrict__ out,
+                         int64_t out_stride) {
+    const int64_t nk4 = (n_params + 3) / 4;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= nk4 * n) return;
+    const int32_t i = (int32_t)(g / nk4);
+    const int64_t k4 = g - (int64_t)i * nk4;
+    float v[4];
+    ask_row4(master, n_params, (float)*sigma, seed, sid, gen, (uint32_t)(i0 + i), k4, v);
+    float* row = out + (int64_t)i * out_stride;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (4 * k4 + q < n_params) row[4 * k4 + q] = v[q];
+}
+
+// first index of the maximum, NaN counting as the maximum (np.argmax)
+__device__ __forceinline__ bool better(double a, int ia, double b, int ib) {
+    const bool na = a != a, nb = b != b;
+    if (na != nb) return na;
+    if (na) return ia < ib;
+    if (a != b) return a > b;
+    return ia < ib;
+}
+
+constexpr int kTellBlock = 256;
+
+__global__ __launch_bounds__(kTellBlock) void k_ga_tell(
+    sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
+    const int32_t* __restrict__ trades, int32_t P, float* __restrict__ master_mm,
+    const float* __restrict__ pop_mm, int64_t pop_mm_stride, float* __restrict__ master_adv,
+    const float* __restrict__ pop_adv, int64_t pop_adv_stride, int64_t n_mm, int64_t n_adv,
+    uint64_t seed, uint32_t gen, sgmm_ga_history* __restrict__ hist) {
+    __shared__ double sv[2][kTellBlock];
+    __shared__ int si[2][kTellBlock];
+    const int tid = threadIdx.x;
+    double bv = 0.0, av = 0.0;
+    int bi = -1, aj = -1;
+    for (int i = tid; i < P; i += kTellBlock) {
+        const double f = fit[i];
+        if (bi < 0 || better(f, i, bv, bi)) { bv = f; bi = i; }
+        if (aj < 0 || better(-f, i, av, aj)) { av = -f; aj = i; }
+    }
+    sv[0][tid] = bv; si[0][tid] = bi;
+    sv[1][tid] = av; si[1][tid] = aj;
+    __syncthreads();
+    for (int w = kTellBlock / 2; w > 0; w >>= 1) {
+        if (tid < w) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int io = si[r][tid + w];
+                if (io >= 0 && (si[r][tid] < 0 || better(sv[r][tid + w], io, sv[r][tid], si[r][tid]))) {
+                    sv[r][tid] = sv[r][tid + w];
+                    si[r][tid] = io;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int best = si[0][0], abest = si[1][0];
+    const double sig_mm = st->sigma_mm, sig_adv = st->sigma_adv;
+    __syncthreads();
+    // new masters (model.py:75): copy the host-supplied row, or regenerate
+    // the ask() of that individual in place (counter-based RNG)
+    const int64_t nk_mm = (n_mm + 3) / 4;
+    for (int64_t k4 = tid; k4 < nk_mm; k4 += kTellBlock) {
+        if (pop_mm) {
+            for (int q = 0; q < 4; ++q)
+                if (4 * k4 + q < n_mm) master_mm[4 * k4 + q] = pop_mm[best * pop_mm_stride + 4 * k4 + q];
+        } else {
+            float v[4];
+            ask_row4(master_mm, n_mm, (float)sig_mm, seed, 0u, gen, (uint32_t)best, k4, v);
+            for (int q = 0; q < 4; ++q)
+                if (4 * k4 + q < n_mm) master_mm[4 * k4 + q] = v[q];
+        }
+    }
+    if (master_adv) {
+        const int64_t nk_adv = (n_adv + 3) / 4;
+        for (int64_t k4 = tid; k4 < nk_adv; k4 += kTellBlock) {
+            if (pop_adv) {
+                for (int q = 0; q < 4; ++q)
+                    if (4 * k4 + q < n_adv) master_adv[4 * k4 + q] = pop_adv[abest * pop_adv_stride + 4 * k4 + q];
+            } else {
+                float v[4];
+                ask_row4(master_adv, n_adv, (float)sig_adv, seed, 1u, gen, (uint32_t)abest, k4, v);
+                for (int q = 0; q < 4; ++q)
+                    if (4 * k4 + q < n_adv) master_adv[4 * k4 + q] = v[q];
+            }
+        }
+    }
+    if (tid == 0) {
+        st->best_idx = best;
+        st->adv_best_idx = abest;
+        st->last_train_f = fit[best];
+        if (hist) {
+            hist->train_f = fit[best];
+            hist->train_trades = trades ? trades[best] : 0;
+            hist->best_idx = best;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kTellBlock) void k_ga_val_update(
+    sgmm_ga_state* __restrict__ st, const double* __restrict__ vfit,
+    const int32_t* __restrict__ vtrades, int32_t use_best, const float* __restrict__ master,
+    float* __restrict__ best_master, int64_t n, sgmm_ga_history* __restrict__ hist) {
+    __shared__ int improved;
+    const int idx = use_best ? st->best_idx : 0;
+    const double v = vfit[idx];
+    if (threadIdx.x == 0) improved = v > st->best_val;  // drl_engine.py:143 (NaN -> False)
+    __syncthreads();
+    if (improved && best_master)
+        for (int64_t k = threadIdx.x; k < n; k += kTellBlock) best_master[k] = master[k];
+    if (threadIdx.x == 0) {
+        int decayed = 0;
+        if (improved) {
+            st->best_val = v;
+            st->no_improve = 0;
+        } else {
+            st->no_improve += 1;
+        }
+        if (st->no_improve >= st->patience) {  // drl_engine.py:155-160
+            st->sigma_mm *= st->decay;
+            st->sigma_adv *= st->decay;
+            st->no_improve = 0;
+            decayed = 1;
+        }
+        st->improved = improved;
+        st->decayed = decayed;
+        st->last_val_f = v;
+        st->gen += 1;
+        if (hist) {
+            hist->val_f = v;
+            hist->val_trades = vtrades ? vtrades[idx] : 0;
+            hist->sigma_after = st->sigma_mm;
+            hist->flags = improved | (decayed << 1);
+        }
+    }
+}
+
+__global__ void k_ga_state_init(sgmm_ga_state* st, double sigma, int32_t patience, double decay) {
+    st->sigma_mm = sigma;
+    st->sigma_adv = sigma;
+    st->best_val = -INFINITY;
+    st->last_train_f = 0.0;
+    st->last_val_f = 0.0;
+    st->no_improve = 0;
+    st->best_idx = -1;
+    st->adv_best_idx = -1;
+    st->gen = 0;
+    st->improved = 0;
+    st->decayed = 0;
+    st->patience = patience;
+    st->pad_ = 0;
+    st->decay = decay;
+}
+
+}  // namespace sgmm
+
+using namespace sgmm;
+
+extern "C" int sgmm_ga_ask(const float* master, int64_t n_params, const double* sigma,
+                           uint64_t seed, uint32_t stream_id, uint32_t gen, int32_t i0, int32_t n,
+                           float* out, int64_t out_stride, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(master && sigma && out, "null pointer");
+    SGMM_REQUIRE(n_params > 0 && n >= 0 && i0 >= 0 && out_stride >= n_params, "bad shape");
+    if (n == 0) return SGMM_OK;
+    const int64_t work = ((n_params + 3) / 4) * (int64_t)n;
+    hipLaunchKernelGGL(k_ga_ask, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
+                       as_stream(stream), master, n_params, sigma, seed, stream_id, gen, i0, n,
+                       out, out_stride);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_ga_state_init(sgmm_ga_state* state, double sigma, int32_t patience,
+                                  double decay, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(state, "null state");
+    hipLaunchKernelGGL(k_ga_state_init, dim3(1), dim3(1), 0, as_stream(stream), state, sigma,
+                       patience, decay);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_ga_tell(sgmm_ga_state* state, const double* fitness, const int32_t* trades,
+                            int32_t P, float* master_mm, const float* pop_mm,
+                            int64_t pop_mm_stride, float* master_adv, const float* pop_adv,
+                            int64_t pop_adv_stride, int64_t n_params_mm, int64_t n_params_adv,
+                            uint64_t seed, uint32_t gen, sgmm_ga_history* history_row,
+                            void* stream) {
+    clear_error();
+    SGMM_REQUIRE(state && fitness && master_mm, "null pointer");
+    SGMM_REQUIRE(P > 0 && n_params_mm > 0, "bad P / n_params_mm");
+    SGMM_REQUIRE(!pop_mm || pop_mm_stride >= n_params_mm, "pop_mm_stride too small");
+    SGMM_REQUIRE(!master_adv || n_params_adv > 0, "n_params_adv");
+    SGMM_REQUIRE(!pop_adv || pop_adv_stride >= n_params_adv, "pop_adv_stride too small");
+    hipLaunchKernelGGL(k_ga_tell, dim3(1), dim3(kTellBlock), 0, as_stream(stream), state,
+                       fitness, trades, P, master_mm, pop_mm, pop_mm_stride, master_adv, pop_adv,
+                       pop_adv_stride, n_params_mm, n_params_adv, seed, gen, history_row);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_ga_val_update(sgmm_ga_state* state, const double* val_fitness,
+                                  const int32_t* val_trades, int32_t use_best_index,
+                                  const float* master_mm, float* best_master, int64_t n_params_mm,
+                                  sgmm_ga_history* history_row, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(state && val_fitness && master_mm, "null pointer");
+    SGMM_REQUIRE(n_params_mm > 0, "n_params_mm");
+    hipLaunchKernelGGL(k_ga_val_update, dim3(1), dim3(kTellBlock), 0, as_stream(stream), state,
+                       val_fitness, val_trades, use_best_index, master_mm, best_master,
+                       n_params_mm, history_row);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}

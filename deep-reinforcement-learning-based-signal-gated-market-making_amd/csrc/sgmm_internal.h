@@ -1,0 +1,47 @@
+// sgmm_internal.h -- host-side helpers shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <string>
+
+#include "../../include/sgmm.h"
+
+namespace sgmm {
+
+void set_error(const char* fmt, ...);
+void clear_error();
+
+#define SGMM_REQUIRE(cond, ...)                     \
+    do {                                            \
+        if (!(cond)) {                              \
+            ::sgmm::set_error(__VA_ARGS__);         \
+            return SGMM_ERR_ARG;                    \
+        }                                           \
+    } while (0)
+
+#define SGMM_HIP(call)                                                              \
+    do {                                                                            \
+        hipError_t err_ = (call);                                                   \
+        if (err_ != hipSuccess) {                                                   \
+            ::sgmm::set_error("%s failed: %s", #call, hipGetErrorString(err_));     \
+            return SGMM_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+#define SGMM_LAUNCHED()                                                             \
+    do {                                                                            \
+        hipError_t err_ = hipGetLastError();                                        \
+        if (err_ != hipSuccess) {                                                   \
+            ::sgmm::set_error("kernel launch failed: %s", hipGetErrorString(err_)); \
+            return SGMM_ERR_HIP;                                                    \
+        }                                                                           \
+    } while (0)
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline bool supported_hidden(int h) { return h == 8 || h == 16 || h == 32 || h == 64; }
+
+}  // namespace sgmm

@@ -1,0 +1,395 @@
+"""Population fitness engine: drop-in for Env/drl_engine.py.
+
+``evaluate_individual``  -- same signature/return as drl_engine.py:9-67.
+``evaluate_population``  -- the batched form of ``pool.starmap(evaluate_individual,
+                            zip(mm_pop, adv_pop))`` (drl_engine.py:104-115).
+``DRLEngine``            -- same constructor / ``train`` signature and results as
+                            drl_engine.py:69-178, with the generation loop
+                            (ask -> rollout -> tell -> validation -> sigma decay)
+                            resident on the GPU.
+
+Every rollout runs in libsgmm.so (HIP, gfx950); without a GPU these functions
+raise -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sys
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import GAHistory, GAState, check, ptr, stream_ptr
+from .model import NeuroEvolution, TradingPolicy, genome_size, genome_to_state_dict, hidden_from_genome
+from .rollout import EnvConfig, EpisodeBatch, RolloutEngine, TickStore, params_tensor
+
+ADV_GENOME = genome_size(32)  # adversary evolver masters are TradingPolicy() genomes (model.py:63)
+
+_engines: dict = {}
+_bundle_cache: "OrderedDict[bytes, TickStore]" = OrderedDict()
+
+
+def _engine(device=None) -> RolloutEngine:
+    dev = torch.device(device or "cuda")
+    if dev not in _engines:
+        _engines[dev] = RolloutEngine(dev)
+    return _engines[dev]
+
+
+def _bundle_key(bundles, train_stats) -> bytes:
+    h = hashlib.blake2b(digest_size=16)
+    for b in bundles:
+        for a in b:
+            a = np.ascontiguousarray(a)
+            h.update(str(a.dtype).encode())
+            h.update(a.tobytes())
+    for k in ("s1_m", "s1_s", "s2_m", "s2_s"):
+        v = train_stats[k]
+        h.update(f"{k}:{type(v).__name__}:{float(v).hex()}".encode())
+    return h.digest()
+
+
+def device_ticks(bundles, train_stats, device=None) -> TickStore:
+    """Upload (and cache) bundles as one SoA TickStore; segment i = bundles[i]."""
+    key = _bundle_key(bundles, train_stats) + str(device).encode()
+    ts = _bundle_cache.get(key)
+    if ts is None:
+        ts = TickStore()
+        for b in bundles:
+            ts.add(b, train_stats)
+        ts.to(torch.device(device or "cuda"))
+        _bundle_cache[key] = ts
+        while len(_bundle_cache) > 8:
+            _bundle_cache.popitem(last=False)
+    else:
+        _bundle_cache.move_to_end(key)
+    return ts
+
+
+def _stack(pop, n_params, device):
+    if torch.is_tensor(pop):
+        t = pop.reshape(-1, n_params)
+    else:
+        t = torch.stack([torch.as_tensor(w, dtype=torch.float32).reshape(-1) for w in pop])
+    return t.to(device=device, dtype=torch.float32).contiguous()
+
+
+def evaluate_population(mm_pop, adv_pop, bundle, phi, tick_size, fee_rate, train_stats,
+                        use_arl=False, device=None):
+    """Fitness of every (mm, adv) pair on one bundle: returns (f64[P], i32[P]).
+
+    ``adv_pop`` may be None or contain None entries (no adversary for that pair),
+    matching ``adv_weights is not None`` in drl_engine.py:16."""
+    eng = _engine(device)
+    dev = eng.device
+    n_mm = len(mm_pop)
+    G = (mm_pop.shape[1] if torch.is_tensor(mm_pop) else len(mm_pop[0]))
+    H = hidden_from_genome(int(G))
+    mm = _stack(mm_pop, G, dev)
+    ticks = device_ticks([bundle], train_stats, dev)
+    off, T = ticks.segments[0]
+    adv = None
+    adv_idx = None
+    if use_arl and adv_pop is not None and any(a is not None for a in adv_pop):
+        rows = [a if a is not None else torch.zeros(ADV_GENOME) for a in adv_pop]
+        Ga = max(len(torch.as_tensor(r).reshape(-1)) for r in rows)
+        adv = torch.zeros((len(rows), Ga), dtype=torch.float32)
+        for i, r in enumerate(rows):
+            r = torch.as_tensor(r, dtype=torch.float32).reshape(-1)
+            adv[i, :len(r)] = r
+        adv = adv.to(dev)
+        adv_idx = np.array([i if a is not None else -1 for i, a in enumerate(adv_pop)], np.int32)
+    eps = EpisodeBatch(genome=np.arange(n_mm), tick_off=np.full(n_mm, off), length=np.full(n_mm, T),
+                       param=np.zeros(n_mm), adv=adv_idx).to(dev)
+    params = params_tensor([EnvConfig(phi=phi, tick_size=tick_size, fee_rate=fee_rate)], dev)
+    fit, trd = eng.fitness(ticks, eps, params, mm, H, adv)
+    return fit.cpu().numpy(), trd.cpu().numpy()
+
+
+def evaluate_individual(mm_weights, adv_weights, bundle, phi, tick_size, fee_rate, train_stats,
+                        use_arl=False):
+    """One episode (drl_engine.py:9-67) on the GPU: returns (total_reward, trades)."""
+    fit, trd = evaluate_population([mm_weights], [adv_weights], bundle, phi, tick_size, fee_rate,
+                                   train_stats, use_arl=use_arl)
+    return np.float64(fit[0]), int(trd[0])
+
+
+def _dist_info(dist):
+    if dist is False:
+        return None, 0, 1
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        g = dist if dist not in (None, True) else None
+        return g, torch.distributed.get_rank(g), torch.distributed.get_world_size(g)
+    return None, 0, 1
+
+
+def shard_bounds(P, rank, world):
+    """Contiguous population shard of a rank: [i0, i1)."""
+    base, rem = divmod(P, world)
+    i0 = rank * base + min(rank, rem)
+    return i0, i0 + base + (1 if rank < rem else 0)
+
+
+class DRLEngine:
+    """Neuroevolution trainer (drl_engine.py:69-178), generation loop on device.
+
+    Reference-compatible arguments; keyword-only extras:
+      hidden_dim  -- TradingPolicy hidden width (reference: 32).
+      rng         -- "device": populations from a counter-based Philox stream on
+                     the GPU (fast, reproducible from ``seed``, identical on every
+                     rank); "torch": the reference's torch CPU generator, so a run
+                     under torch.manual_seed reproduces the reference's trajectory.
+      seed        -- device RNG seed (default: drawn from the torch generator).
+      val_mode    -- "fused": validate every individual in the training launch and
+                     pick the best's value (removes a serial episode per generation);
+                     "best": validate only the best after tell (reference order);
+                     "auto": fused for shards of <= 512 individuals.
+      honor_sigma -- the reference ignores DRLEngine(sigma=...) (NeuroEvolution keeps
+                     its 0.05 default, drl_engine.py:77); True uses it.
+      sync_every  -- generations between host synchronisations (log lines and
+                     checkpoint writes are emitted at these points, in order).
+      dist        -- torch.distributed group (None = default if initialised,
+                     False = single process): the population is sharded over ranks
+                     and fitness is all-gathered once per generation.
+    """
+
+    def __init__(self, pop_size=50, sigma=0.05, phi=0.01, tick_size=0.01, fee_rate=0.0,
+                 use_arl=False, save_dir="checkpoints/drl", *, hidden_dim=32, rng="device",
+                 seed=None, val_mode="auto", honor_sigma=False, sync_every=10, dist=None,
+                 device=None, verbose=True, patience=15, decay=0.5):
+        self.phi = phi
+        self.tick_size = tick_size
+        self.fee_rate = fee_rate
+        self.save_dir = save_dir
+        os.makedirs(self.save_dir, exist_ok=True)
+        self.use_arl = use_arl
+        self.pop_size = int(pop_size)
+        self.hidden_dim = int(hidden_dim)
+        self.mm_evolver = NeuroEvolution(population_size=pop_size, hidden_dim=self.hidden_dim)
+        if honor_sigma:
+            self.mm_evolver.sigma = sigma
+        if use_arl:
+            self.adv_evolver = NeuroEvolution(population_size=pop_size)
+            if honor_sigma:
+                self.adv_evolver.sigma = sigma
+        if rng not in ("device", "torch"):
+            raise ValueError("rng must be 'device' or 'torch'")
+        self.rng = rng
+        self.seed = int(seed) if seed is not None else int(torch.randint(0, 2**62, (1,)).item()) \
+            if rng == "device" else 0
+        self.val_mode = val_mode
+        self.sync_every = max(1, int(sync_every))
+        self.dist = dist
+        self.device = device
+        self.verbose = verbose
+        self.patience = int(patience)
+        self.decay = float(decay)
+        self.timing = {}
+
+    # ------------------------------------------------------------------ helpers
+    def _log(self, msg):
+        if self.verbose:
+            print(msg)
+            sys.stdout.flush()
+
+    def train(self, train_bundle, val_bundle, train_stats, generations=100, output_prefix="agent"):
+        _lib.require_gpu()
+        eng = _engine(self.device)
+        dev = eng.device
+        L = eng.L
+        group, rank, world = _dist_info(self.dist)
+        P, H = self.pop_size, self.hidden_dim
+        G = genome_size(H)
+        i0, i1 = shard_bounds(P, rank, world)
+        n_loc = i1 - i0
+        arl = self.use_arl
+        fused = self.val_mode == "fused" or (self.val_mode == "auto" and n_loc <= 512)
+        torch_rng = self.rng == "torch"
+        # (rng="torch" with world > 1: every rank draws the identical full
+        # population from its identically seeded generator)
+
+        ticks = device_ticks([train_bundle, val_bundle], train_stats, dev)
+        (tr_off, T_tr), (va_off, T_va) = ticks.segments
+        params = params_tensor([EnvConfig(phi=self.phi, tick_size=self.tick_size,
+                                          fee_rate=self.fee_rate)], dev)
+        # episode batches: training shard (+ fused validation of the shard)
+        if fused and not arl:
+            train_eps = EpisodeBatch(np.concatenate([np.arange(n_loc), np.arange(n_loc)]),
+                                     np.concatenate([np.full(n_loc, tr_off), np.full(n_loc, va_off)]),
+                                     np.concatenate([np.full(n_loc, T_tr), np.full(n_loc, T_va)]),
+                                     np.zeros(2 * n_loc)).to(dev)
+            val_eps = None
+        else:
+            train_eps = EpisodeBatch(np.arange(n_loc), np.full(n_loc, tr_off), np.full(n_loc, T_tr),
+                                     np.zeros(n_loc), adv=np.arange(n_loc) if arl else None).to(dev)
+            nv = n_loc if fused else 1
+            val_eps = EpisodeBatch(np.arange(nv), np.full(nv, va_off), np.full(nv, T_va), np.zeros(nv)).to(dev)
+
+        f32 = dict(dtype=torch.float32, device=dev)
+        pop = torch.empty((P if torch_rng else n_loc, G), **f32)
+        pop_loc = pop[i0:i1] if torch_rng else pop
+        adv_pop = torch.empty((P if torch_rng else n_loc, ADV_GENOME), **f32) if arl else None
+        adv_loc = (adv_pop[i0:i1] if torch_rng else adv_pop) if arl else None
+        master = self.mm_evolver.master_policy.get_weights().to(**f32)
+        master_adv = self.adv_evolver.master_policy.get_weights().to(**f32) if arl else None
+        best_master = torch.zeros(G, **f32)
+        state = torch.zeros(ctypes_size(GAState), dtype=torch.uint8, device=dev)
+        hist = torch.zeros((generations, ctypes_size(GAHistory)), dtype=torch.uint8, device=dev)
+        n_out = train_eps.n
+        out = (torch.empty(n_out, dtype=torch.float64, device=dev),
+               torch.empty(n_out, dtype=torch.int32, device=dev))
+        vout = (torch.empty(val_eps.n, dtype=torch.float64, device=dev),
+                torch.empty(val_eps.n, dtype=torch.int32, device=dev)) if val_eps is not None else None
+        # full-population views (gathered when world > 1)
+        n_max = shard_bounds(P, 0, world)[1]
+        gbuf = torch.empty((world, 4, n_max), dtype=torch.float64, device=dev) if world > 1 else None
+        s = stream_ptr()
+        check(L.sgmm_ga_state_init(ptr(state), float(self.mm_evolver.sigma), self.patience, self.decay, s),
+              "sgmm_ga_state_init")
+        if arl and self.adv_evolver.sigma != self.mm_evolver.sigma:
+            raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
+        sig_mm = ptr(state)  # sigma_mm is the first field of sgmm_ga_state
+        sig_adv = ctypes_offset_ptr(state, GAState.sigma_adv.offset)
+        best_path = os.path.join(self.save_dir, f"{output_prefix}_best_val_{self.phi}.pth")
+        saved_any = False
+        emitted = 0
+        history = {"gen": [], "train_f": [], "val_f": [], "train_trades": [], "val_trades": []}
+        ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev_start.record()
+
+        def flush(upto):
+            nonlocal emitted, saved_any
+            if upto <= emitted:
+                return
+            rows = hist[emitted:upto].cpu().numpy().view(HIST_DTYPE).reshape(-1)
+            improved_any = False
+            for k, r in enumerate(rows):
+                g = emitted + k
+                imp = bool(r["flags"] & 1)
+                improved_any |= imp
+                if r["flags"] & 2:
+                    self._log(f">>> Sigma decayed to {r['sigma_after']:.4f} due to no improvement")
+                history["gen"].append(g)
+                history["train_f"].append(np.float64(r["train_f"]))
+                history["val_f"].append(np.float64(r["val_f"]))
+                history["train_trades"].append(int(r["train_trades"]))
+                history["val_trades"].append(int(r["val_trades"]))
+                if g % 5 == 0:
+                    tag = "ARL:ON" if arl else "ARL:OFF"
+                    self._log(f"Gen {g:03d} | {tag} | Best Train: {r['train_f']:.2f} | "
+                              f"Val: {r['val_f']:.2f}{'*' if imp else ''}")
+            if improved_any and rank == 0:
+                torch.save(genome_to_state_dict(best_master, H), best_path)
+            saved_any |= improved_any
+            emitted = upto
+
+        for gen in range(generations):
+            # 1. ask (models/model.py:65-71)
+            if torch_rng:
+                st_now = state.cpu().numpy().view(STATE_DTYPE)[0]
+                pop.copy_(_host_ask(master, float(st_now["sigma_mm"]), P))
+                if arl:
+                    adv_pop.copy_(_host_ask(master_adv, float(st_now["sigma_adv"]), P))
+            else:
+                check(L.sgmm_ga_ask(ptr(master), G, sig_mm, self.seed, 0, gen, i0, n_loc, ptr(pop), G, s),
+                      "sgmm_ga_ask")
+                if arl:
+                    check(L.sgmm_ga_ask(ptr(master_adv), ADV_GENOME, sig_adv, self.seed, 1, gen, i0, n_loc,
+                                        ptr(adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
+            # 2. rollout of the shard (drl_engine.py:104-115)
+            eng.fitness(ticks, train_eps, params, pop_loc, H, adv_loc, out=out)
+            if fused and val_eps is not None:
+                eng.fitness(ticks, val_eps, params, pop_loc, H, None, out=vout)
+            if fused and not arl:
+                tr_f, tr_t, va_f, va_t = out[0][:n_loc], out[1][:n_loc], out[0][n_loc:], out[1][n_loc:]
+            elif fused:
+                tr_f, tr_t, va_f, va_t = out[0], out[1], vout[0], vout[1]
+            else:
+                tr_f, tr_t, va_f, va_t = out[0], out[1], None, None
+            # 3. all-gather the shards' fitness (one collective per generation)
+            if world > 1:
+                tr_f, tr_t, va_f, va_t = _gather(gbuf, tr_f, tr_t, va_f, va_t, P, world, group)
+            # 4. tell both evolvers (model.py:73-76, drl_engine.py:119-125)
+            check(L.sgmm_ga_tell(ptr(state), ptr(tr_f), ptr(tr_t), P, ptr(master),
+                                 ptr(pop) if torch_rng else None, G,
+                                 ptr(master_adv) if arl else None,
+                                 ptr(adv_pop) if (arl and torch_rng) else None, ADV_GENOME, G,
+                                 ADV_GENOME if arl else 0, self.seed, gen,
+                                 ctypes_offset_ptr(hist, gen * HIST_DTYPE.itemsize), s), "sgmm_ga_tell")
+            # 5. validation of the best (drl_engine.py:129-140)
+            if not fused:
+                eng.fitness(ticks, val_eps, params, master.view(1, G), H, None, out=vout)
+                va_f, va_t = vout
+            check(L.sgmm_ga_val_update(ptr(state), ptr(va_f), ptr(va_t), 1 if fused else 0, ptr(master),
+                                       ptr(best_master), G, ctypes_offset_ptr(hist, gen * HIST_DTYPE.itemsize),
+                                       s), "sgmm_ga_val_update")
+            if torch_rng:
+                TradingPolicy()  # the reference's validation builds a TradingPolicy() (RNG draw)
+            if (gen + 1) % self.sync_every == 0:
+                flush(gen + 1)
+        ev_end.record()
+        flush(generations)
+        torch.cuda.synchronize()
+        self.timing = {"generations": generations, "ms": ev_start.elapsed_time(ev_end),
+                       "env_steps": generations * P * T_tr}
+        st = state.cpu().numpy().view(STATE_DTYPE)[0]
+        self.mm_evolver.sigma = float(st["sigma_mm"])
+        self.mm_evolver.master_policy.set_weights(master.cpu())
+        if arl:
+            self.adv_evolver.sigma = float(st["sigma_adv"])
+            self.adv_evolver.master_policy.set_weights(master_adv.cpu())
+        # reload the best-validation weights (drl_engine.py:174-176)
+        if saved_any:
+            self.mm_evolver.master_policy.load_state_dict(genome_to_state_dict(best_master, H))
+        elif os.path.exists(best_path):
+            self.mm_evolver.master_policy.load_state_dict(torch.load(best_path, weights_only=True))
+        return self.mm_evolver.master_policy, history
+
+
+# ---------------------------------------------------------------------- small helpers
+def ctypes_size(t):
+    import ctypes
+    return ctypes.sizeof(t)
+
+
+def ctypes_offset_ptr(tensor, offset):
+    import ctypes
+    return ctypes.c_void_p(tensor.data_ptr() + int(offset))
+
+
+HIST_DTYPE = np.dtype([("train_f", "<f8"), ("val_f", "<f8"), ("sigma_after", "<f8"),
+                       ("train_trades", "<i4"), ("val_trades", "<i4"), ("best_idx", "<i4"),
+                       ("flags", "<i4")])
+STATE_DTYPE = np.dtype([("sigma_mm", "<f8"), ("sigma_adv", "<f8"), ("best_val", "<f8"),
+                        ("last_train_f", "<f8"), ("last_val_f", "<f8"), ("no_improve", "<i4"),
+                        ("best_idx", "<i4"), ("adv_best_idx", "<i4"), ("gen", "<i4"),
+                        ("improved", "<i4"), ("decayed", "<i4"), ("patience", "<i4"),
+                        ("pad_", "<i4"), ("decay", "<f8")])
+assert HIST_DTYPE.itemsize == ctypes_size(GAHistory) and STATE_DTYPE.itemsize == ctypes_size(GAState)
+
+
+def _host_ask(master_dev, sigma, P):
+    """NeuroEvolution.ask on the torch CPU generator (reference stream), uploaded."""
+    m = master_dev.cpu()
+    return torch.stack([m + torch.randn_like(m) * sigma for _ in range(P)]).to(master_dev.device)
+
+
+def _gather(gbuf, tr_f, tr_t, va_f, va_t, P, world, group):
+    n_max = gbuf.shape[2]
+    n = tr_f.shape[0]
+    mine = torch.zeros((4, n_max), dtype=torch.float64, device=tr_f.device)
+    mine[0, :n] = tr_f
+    mine[1, :n] = tr_t.to(torch.float64)
+    if va_f is not None:
+        mine[2, :n] = va_f
+        mine[3, :n] = va_t.to(torch.float64)
+    torch.distributed.all_gather_into_tensor(gbuf, mine, group=group)
+    counts = [shard_bounds(P, r, world)[1] - shard_bounds(P, r, world)[0] for r in range(world)]
+    parts = [gbuf[r, :, :counts[r]] for r in range(world)]
+    full = torch.cat(parts, dim=1)
+    out_va_f = full[2].contiguous() if va_f is not None else None
+    out_va_t = full[3].to(torch.int32) if va_f is not None else None
+    return full[0].contiguous(), full[1].to(torch.int32), out_va_f, out_va_t

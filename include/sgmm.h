@@ -1,0 +1,225 @@
+/*
+ * sgmm.h -- C ABI of the MI355X population-rollout library (libsgmm.so).
+ *
+ * Drop-in boundary for the hot path of the reference repository
+ * (KAS-W/Deep-Reinforcement-Learning-Based-Signal-Gated-Market-Making).
+ * The reference has no FFI: its boundary is a set of Python call signatures.
+ * Each entry point below names the reference interface it replaces
+ * (paths relative to the reference root); INTEGRATION.md shows the
+ * Python (ctypes) binding a maintainer adds on the reference side.
+ *
+ * Conventions
+ *   - Every pointer argument is caller-owned DEVICE memory (hipMalloc / torch
+ *     CUDA tensors) unless stated otherwise.  No entry point allocates, frees
+ *     or synchronises in the hot calls: work is enqueued on `stream`
+ *     (a hipStream_t, NULL = default stream) and the call returns.
+ *   - Return value: 0 = success, < 0 = error; sgmm_last_error() (thread-local)
+ *     describes the last failure.  Argument errors are detected before any
+ *     work is enqueued.
+ *   - Calls on distinct streams are thread-safe.
+ *   - Numerics: prices/cash/reward float64 without FMA contraction (the
+ *     reference's operation order, market_env.py:30-58); policy MLP float32
+ *     with each dot product evaluated as the k-ordered fused chain starting at
+ *     the bias; actions = rint(raw * act_scale) (round half to even, np.round).
+ */
+#ifndef SGMM_H
+#define SGMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGMM_ABI_VERSION 1
+
+enum {
+    SGMM_OK = 0,
+    SGMM_ERR_ARG = -1,       /* invalid argument (shape, pointer, range) */
+    SGMM_ERR_HIP = -2,       /* HIP runtime error */
+    SGMM_ERR_WORKSPACE = -3, /* workspace too small */
+    SGMM_ERR_UNSUPPORTED = -4
+};
+
+/* Per-episode environment constants.
+ * FTPEnv.__init__ (Env/market_env.py:8-15) plus the constants
+ * evaluate_individual hard-codes (Env/drl_engine.py:39,48,64-65). */
+typedef struct sgmm_env_params {
+    double  phi;          /* inventory penalty lambda (market_env.py:10) */
+    double  tick;         /* tick size (market_env.py:11) */
+    double  fee;          /* fee rate (market_env.py:9) */
+    double  idle_penalty; /* subtracted from fitness if no trade (drl_engine.py:64-65): 50.0 */
+    int32_t i_max;        /* inventory cap (market_env.py:14): 2 */
+    int32_t i_min;        /* inventory floor (market_env.py:15): -2 */
+    float   act_scale;    /* MM action scale (drl_engine.py:39): 5.0 */
+    float   adv_scale;    /* adversary action scale (drl_engine.py:48): 1.0 */
+} sgmm_env_params;        /* 48 bytes */
+
+/* The bundle (drl_engine.py:11) as structure-of-arrays device columns,
+ * indexed by absolute tick index.  (sgmm_ticks and sgmm_episodes are HOST
+ * structs whose members point to device memory.)  s1n/s2n are the normalised signals of
+ * drl_engine.py:33-34 (host computes them once per bundle). */
+typedef struct sgmm_ticks {
+    const float  *s1n;
+    const float  *s2n;
+    const double *mid_next;
+    const double *best_ask;
+    const double *best_bid;
+    const double *buy_max;
+    const double *sell_min;
+} sgmm_ticks;
+
+/* A batch of episodes: episode e runs genome row genome[e] (and adversary
+ * row adv[e], or -1 for none) over ticks [tick_off[e], tick_off[e]+len[e])
+ * with params[param[e]].  step_off = exclusive prefix sum of len (it places
+ * each episode's tables in the workspace); total_steps = sum of len.
+ * Every episode of one call shares the inventory range [inv_min, inv_max]
+ * (at most 8 inventory values; 0 must lie inside). */
+typedef struct sgmm_episodes {
+    int32_t        n;
+    int32_t        max_len;
+    int64_t        total_steps;
+    int32_t        inv_min;   /* host copy of the (shared) i_min of params */
+    int32_t        inv_max;   /* host copy of the (shared) i_max of params */
+    const int32_t *genome;
+    const int32_t *adv;       /* may be NULL (no adversary anywhere) */
+    const int64_t *tick_off;
+    const int32_t *len;
+    const int64_t *step_off;
+    const int32_t *param;
+} sgmm_episodes;
+
+int         sgmm_abi_version(void);
+const char *sgmm_last_error(void);
+
+/* Batched FTPEnv.step over n independent environments.
+ * Replaces Env/market_env.py:22-67 (FTPEnv.step).  inventory/cash are
+ * updated in place; adv_action may be NULL (no adversary); reward / pnl /
+ * inv_reward / fee_paid / fill_* outputs may individually be NULL.
+ * params: device array, param_idx[n] (NULL = all use params[0]). */
+int sgmm_env_step_batch(const sgmm_env_params *params, const int32_t *param_idx,
+                        int32_t *inventory, double *cash,
+                        const int32_t *action, const int32_t *adv_action,
+                        const double *mid_next, const double *best_ask, const double *best_bid,
+                        const double *buy_max, const double *sell_min,
+                        double *reward, double *pnl_reward, double *inventory_reward,
+                        double *fee_paid, uint8_t *fill_buy, uint8_t *fill_sell,
+                        int64_t n, void *stream);
+
+/* Batched TradingPolicy.forward (models/model.py:267-269): out[i] =
+ * MLP(genomes[genome_idx[i]], states[i]).  Genome layout = parameters()
+ * order W1[H,3] b1[H] W2[H,H] b2[H] W3[2,H] b3[2] (H*H+7H+2 floats).
+ * genome_idx may be NULL (row i).  hidden in {8,16,32,64}. */
+int sgmm_policy_forward(const float *genomes, int64_t genome_stride, int32_t hidden,
+                        const int32_t *genome_idx, const float *states, float *out,
+                        int64_t n, void *stream);
+
+/* Batched AdversaryPolicy.forward (models/model.py:292-293): tanh outputs,
+ * weights = the first 74 floats of each genome row (model.py:295-300). */
+int sgmm_adversary_forward(const float *genomes, int64_t genome_stride,
+                           const int32_t *genome_idx, const float *states, float *out,
+                           int64_t n, void *stream);
+
+/* Workspace bytes sgmm_rollout_fitness needs for this batch. */
+size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps, int32_t n_states);
+
+/* THE HOT PATH.  Fitness of every episode of the batch:
+ * replaces Env/drl_engine.py:9-67 (evaluate_individual) as mapped by
+ * Pool.starmap over the population (drl_engine.py:104-115).
+ * fitness[e] = sum of step rewards (sequential float64 order), minus
+ * idle_penalty if the episode never traded; trades[e] = steps with a fill.
+ * adv_genomes may be NULL (no adversary, eps->adv ignored). */
+int sgmm_rollout_fitness(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                         const sgmm_env_params *params,
+                         const float *mm_genomes, int64_t mm_stride, int32_t hidden,
+                         const float *adv_genomes, int64_t adv_stride,
+                         double *fitness, int32_t *trades,
+                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* Per-step trace of every episode (the recorder loop of
+ * pipeline/agent_trainer.py:144-153 / main.py:63-90 / pipeline/evaluator.py:25-37,
+ * batched).  Outputs are indexed by step_off[e] + t; any may be NULL.
+ * off_a/off_b: MM action before the adversary; adv_a/adv_b: adversary deltas;
+ * inventory/cash: after the step.  Also writes fitness/trades. */
+int sgmm_rollout_trace(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                       const sgmm_env_params *params,
+                       const float *mm_genomes, int64_t mm_stride, int32_t hidden,
+                       const float *adv_genomes, int64_t adv_stride,
+                       int32_t *off_a, int32_t *off_b, int32_t *adv_a, int32_t *adv_b,
+                       int32_t *inventory, double *cash, double *reward, double *pnl_reward,
+                       double *fee_paid, uint8_t *fill_buy, uint8_t *fill_sell,
+                       float *raw_a, float *raw_b,
+                       double *fitness, int32_t *trades, void *stream);
+
+/* NeuroEvolution.ask (models/model.py:65-71) on device:
+ * out[i,k] = master[k] + z(seed, stream_id, gen, i0+i, k) * (float)(*sigma),
+ * z ~ N(0,1) from Philox4x32-10 + Box-Muller (counter-based, so any rank can
+ * regenerate any individual).  sigma is a DEVICE pointer (the evolver's
+ * sigma lives in sgmm_ga_state and decays on device).  out row stride
+ * out_stride. */
+int sgmm_ga_ask(const float *master, int64_t n_params, const double *sigma,
+                uint64_t seed, uint32_t stream_id, uint32_t gen, int32_t i0, int32_t n,
+                float *out, int64_t out_stride, void *stream);
+
+/* Device GA bookkeeping state (DRLEngine.train locals, drl_engine.py:84-89,
+ * 143-160).  Initialise with sgmm_ga_state_init. */
+typedef struct sgmm_ga_state {
+    double  sigma_mm;      /* NeuroEvolution.sigma of the MM evolver */
+    double  sigma_adv;     /* ... of the adversary evolver */
+    double  best_val;      /* best_val_reward (-inf at start) */
+    double  last_train_f;  /* best train fitness of the last generation */
+    double  last_val_f;    /* validation reward of the last generation */
+    int32_t no_improve;    /* no_improvement_gens */
+    int32_t best_idx;      /* argmax of the last generation */
+    int32_t adv_best_idx;  /* argmax of -fitness (adversary tell) */
+    int32_t gen;           /* generations completed */
+    int32_t improved;      /* last generation improved the validation reward */
+    int32_t decayed;       /* last generation decayed sigma */
+    int32_t patience;      /* 15 (drl_engine.py:155) */
+    int32_t pad_;
+    double  decay;         /* 0.5 (drl_engine.py:156) */
+} sgmm_ga_state;           /* 80 bytes */
+
+/* History row written per generation (drl_engine.py:163-167). */
+typedef struct sgmm_ga_history {
+    double  train_f;
+    double  val_f;
+    double  sigma_after;
+    int32_t train_trades;
+    int32_t val_trades;
+    int32_t best_idx;
+    int32_t flags;         /* bit0 improved (checkpoint saved), bit1 sigma decayed */
+} sgmm_ga_history;         /* 40 bytes */
+
+int sgmm_ga_state_init(sgmm_ga_state *state, double sigma, int32_t patience, double decay,
+                       void *stream);
+
+/* NeuroEvolution.tell for both evolvers (model.py:73-76, drl_engine.py:119-125):
+ * best = first index of max(fitness) (np.argmax; NaN counts as max),
+ * adv_best = first index of max(-fitness).  The new master rows are written
+ * into master_mm / master_adv either by copying row best of `pop_mm` /
+ * `pop_adv` (host-supplied populations, may be NULL) or, when the pop
+ * pointer is NULL, by regenerating the ask() of that index in place
+ * (same seed/stream/gen as the ask).  P = global population size. */
+int sgmm_ga_tell(sgmm_ga_state *state, const double *fitness, const int32_t *trades, int32_t P,
+                 float *master_mm, const float *pop_mm, int64_t pop_mm_stride,
+                 float *master_adv, const float *pop_adv, int64_t pop_adv_stride,
+                 int64_t n_params_mm, int64_t n_params_adv,
+                 uint64_t seed, uint32_t gen, sgmm_ga_history *history_row, void *stream);
+
+/* Validation bookkeeping after the best individual's validation rollout
+ * (drl_engine.py:129-171): val_fitness/val_trades are read at index
+ * val_index (the best of this generation when val was evaluated for the
+ * whole population, or 0).  On improvement master_mm is copied to
+ * best_master (the checkpoint slot).  Applies sigma decay. */
+int sgmm_ga_val_update(sgmm_ga_state *state, const double *val_fitness,
+                       const int32_t *val_trades, int32_t use_best_index,
+                       const float *master_mm, float *best_master, int64_t n_params_mm,
+                       sgmm_ga_history *history_row, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SGMM_H */

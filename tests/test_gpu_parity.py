@@ -1,0 +1,237 @@
+"""GPU parity: every HIP entry point against the CPU oracle and the reference's
+golden vectors.  Integer/state outputs (actions, inventories, fills, trades)
+must be bit-exact; float64 cash/reward/fitness are bit-exact too (the kernels
+keep the reference's operation order and sequential summation).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import episodes_from_fixture, has_gpu, stats_dict
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+DEV = torch.device("cuda:0")
+
+
+def _run_batch(sgmm, episodes, arl, trace=False):
+    """Run a list of fixture-style episodes (same H) through the C ABI."""
+    H = episodes[0]["H"]
+    G = H * H + 7 * H + 2
+    ticks = sgmm.TickStore()
+    segs = []
+    for ep in episodes:
+        st = stats_dict(ep["stats"], ep["stats_nb"]) if "stats" in ep else ep["train_stats"]
+        segs.append(ticks.add((ep["s1"], ep["s2"], ep["mid"], ep["ask"], ep["bid"], ep["buy_max"],
+                               ep["sell_min"]), st))
+    ticks.to(DEV)
+    cfgs = [sgmm.EnvConfig(phi=ep["phi"], tick_size=ep["tick"], fee_rate=ep["fee"]) for ep in episodes]
+    params = sgmm.params_tensor(cfgs, DEV)
+    n = len(episodes)
+    mm = torch.from_numpy(np.stack([ep["mm"][:G] for ep in episodes]).astype(np.float32)).to(DEV)
+    adv = None
+    adv_idx = None
+    if arl:
+        adv = torch.from_numpy(np.stack([ep["adv"] if ep["adv"] is not None else np.zeros(1250, np.float32)
+                                         for ep in episodes])).to(DEV)
+        adv_idx = np.array([i if ep["adv"] is not None else -1 for i, ep in enumerate(episodes)])
+    eps = sgmm.EpisodeBatch(np.arange(n), [ticks.segments[s][0] for s in segs],
+                            [ticks.segments[s][1] for s in segs], np.arange(n), adv=adv_idx).to(DEV)
+    eng = sgmm.RolloutEngine(DEV)
+    if trace:
+        return eng.trace(ticks, eps, params, mm, H, adv), eps
+    return eng.fitness(ticks, eps, params, mm, H, adv), eps
+
+
+def _oracle_eval(oracle, ep, trace=False):
+    p = oracle.params(phi=ep["phi"], tick=ep["tick"], fee=ep["fee"])
+    return oracle.evaluate(ep["mm"], ep["H"], ep["adv"], ep["s1n"], ep["s2n"], ep["mid"], ep["ask"],
+                           ep["bid"], ep["buy_max"], ep["sell_min"], p, trace=trace)
+
+
+def _groups(eps):
+    g = {}
+    for ep in eps:
+        g.setdefault((ep["H"], ep["adv"] is not None), []).append(ep)
+    return g
+
+
+@pytest.mark.parametrize("name", ["g2_synthetic.npz", "g3_adversary.npz"])
+def test_fitness_matches_oracle(golden, sgmm, oracle, name):
+    eps = list(episodes_from_fixture(golden(name)))
+    for (H, arl), group in _groups(eps).items():
+        (fit, trd), _ = _run_batch(sgmm, group, arl)
+        fit, trd = fit.cpu().numpy(), trd.cpu().numpy()
+        for i, ep in enumerate(group):
+            f, t = _oracle_eval(oracle, ep)
+            assert trd[i] == t, (name, ep["e"])
+            assert fit[i] == f, (name, ep["e"], fit[i], f)
+
+
+@pytest.mark.parametrize("name", ["g2_synthetic.npz", "g3_adversary.npz"])
+def test_trace_matches_oracle(golden, sgmm, oracle, name):
+    eps = list(episodes_from_fixture(golden(name)))
+    for (H, arl), group in _groups(eps).items():
+        (fit, trd, tr), eb = _run_batch(sgmm, group, arl, trace=True)
+        tr = {k: v.cpu().numpy() for k, v in tr.items()}
+        for i, ep in enumerate(group):
+            f, t, want = _oracle_eval(oracle, ep, trace=True)
+            sl = slice(int(eb.step_off[i]), int(eb.step_off[i]) + len(ep["mid"]))
+            for k in want:
+                assert np.array_equal(tr[k][sl], want[k]), (name, ep["e"], k)
+            assert fit[i].item() == f and trd[i].item() == t
+
+
+def test_g1_real_episode_actions(golden, sgmm):
+    """ARL checkpoint on the recorded 510300 OOS episode (960 steps)."""
+    d = golden("g1_arl_real.npz")
+    ep = dict(H=32, mm=d["genome"], adv=None, s1=d["s1_pred"], s2=d["s2_pred"], mid=d["mid"],
+              ask=d["ask"], bid=d["bid"], buy_max=d["buy_max"], sell_min=d["sell_min"], phi=0.0001,
+              tick=0.001, fee=0.0, stats=d["stats"], stats_nb=True)
+    (fit, trd, tr), _ = _run_batch(sgmm, [ep], False, trace=True)
+    tr = {k: v.cpu().numpy() for k, v in tr.items()}
+    for k in ("off_a", "off_b", "inventory", "fill_buy", "fill_sell", "cash", "reward"):
+        assert np.array_equal(tr[k], d[k]), k
+    assert fit[0].item() == float(d["fitness"]) and trd[0].item() == int(d["trades"])
+    (fit2, trd2), _ = _run_batch(sgmm, [ep], False)
+    assert fit2[0].item() == float(d["fitness"]) and trd2[0].item() == int(d["trades"])
+
+
+def test_env_step_batch_edge_cases(golden, sgmm):
+    d = golden("g4_ties.npz")
+    n = len(d["mid"])
+    env = sgmm.FTPEnvBatch(n, phi=d["phi"], tick_size=d["tick"], fee_rate=d["fee"], device=DEV)
+    env.inventory.copy_(torch.from_numpy(d["inv_before"].astype(np.int32)))
+    env.cash.copy_(torch.from_numpy(d["cash_before"]))
+    act = np.stack([d["off_a"], d["off_b"]], 1)
+    adv = np.stack([d["adv_a"], d["adv_b"]], 1)
+    # rows without an adversary carry zero deltas: identical to adv_action=None
+    r, info = env.step(act, d["mid"], d["ask"], d["bid"], d["buy_max"], d["sell_min"], adv_action=adv)
+    assert np.array_equal(env.inventory.cpu().numpy(), d["inventory"])
+    assert np.array_equal(env.cash.cpu().numpy(), d["cash"])
+    assert np.array_equal(r.cpu().numpy(), d["reward"])
+    assert np.array_equal(info["pnl_reward"].cpu().numpy(), d["pnl"])
+    assert np.array_equal(info["inventory_reward"].cpu().numpy(), d["inv_reward"])
+    assert np.array_equal(info["fee_paid"].cpu().numpy(), d["fee_paid"])
+    assert np.array_equal(info["fill_buy"].cpu().numpy(), d["fill_buy"])
+    assert np.array_equal(info["fill_sell"].cpu().numpy(), d["fill_sell"])
+
+
+@pytest.mark.parametrize("H", [8, 16, 32, 64])
+def test_policy_forward_bit_exact(sgmm, oracle, H):
+    rng = np.random.default_rng(H)
+    G = H * H + 7 * H + 2
+    genomes = (rng.standard_normal((7, G)) * 0.4).astype(np.float32)
+    n = 500
+    idx = rng.integers(0, 7, n).astype(np.int32)
+    states = np.stack([rng.standard_normal(n), rng.standard_normal(n),
+                       rng.integers(-2, 3, n) / 2.0], 1).astype(np.float32)
+    out = sgmm.policy_forward(torch.from_numpy(genomes).to(DEV), H, torch.from_numpy(states).to(DEV),
+                              torch.from_numpy(idx).to(DEV)).cpu().numpy()
+    want = np.stack([oracle.policy_forward(genomes[idx[i]], H, states[i]) for i in range(n)])
+    assert np.array_equal(out, want)
+    # and against the reference-shaped torch module within fp32 ordering slack
+    pol = sgmm.TradingPolicy(hidden_dim=H)
+    pol.set_weights(torch.from_numpy(genomes[0]))
+    ref = pol(torch.from_numpy(states[idx == 0])).numpy()
+    np.testing.assert_allclose(out[idx == 0], ref, rtol=1e-5, atol=1e-5)
+
+
+def test_adversary_forward(sgmm, oracle):
+    rng = np.random.default_rng(1)
+    genomes = (rng.standard_normal((5, 1250)) * 3).astype(np.float32)
+    n = 200
+    idx = rng.integers(0, 5, n).astype(np.int32)
+    states = np.stack([rng.integers(-2, 3, n) / 2.0, rng.integers(0, 2, n), rng.integers(0, 2, n)], 1).astype(np.float32)
+    out = sgmm.adversary_forward(torch.from_numpy(genomes).to(DEV), torch.from_numpy(states).to(DEV),
+                                 torch.from_numpy(idx).to(DEV)).cpu().numpy()
+    want = np.stack([oracle.adversary_forward(genomes[idx[i]], states[i]) for i in range(n)])
+    np.testing.assert_allclose(out, want, rtol=0, atol=2e-7)  # tanhf: ocml vs glibc, <= 1 ulp
+    assert np.array_equal(np.rint(out), np.rint(want))
+
+
+def _synthetic_batch(sgmm, P, T, H, seed, lengths=None, phi=0.001, nan_frac=0.0, sigma=0.3):
+    from sgmm_amd import synthetic
+    b = synthetic.bundle_510300(T, seed=seed, nan_frac=nan_frac)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=sigma, seed=seed + 1).numpy()
+    lens = np.full(P, T) if lengths is None else np.asarray(lengths)
+    eps = []
+    for i in range(P):
+        L = int(lens[i])
+        s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+        eps.append(dict(H=H, mm=pop[i], adv=None, s1=b[0][:L], s2=b[1][:L], s1n=s1n[:L], s2n=s2n[:L],
+                        mid=b[2][:L], ask=b[3][:L], bid=b[4][:L], buy_max=b[5][:L], sell_min=b[6][:L],
+                        phi=phi, tick=0.001, fee=0.0, train_stats=st))
+    return eps
+
+
+def test_ragged_lengths_and_segment_boundaries(sgmm, oracle):
+    """Lengths around the 64-tick chunk, 256-tick table block and 4096-tick
+    summation segment boundaries, plus zero-length episodes."""
+    lens = [0, 1, 63, 64, 65, 255, 256, 257, 4095, 4096, 4097, 9000]
+    eps = _synthetic_batch(sgmm, len(lens), max(lens), 16, seed=11, lengths=lens)
+    (fit, trd), _ = _run_batch(sgmm, eps, False)
+    fit, trd = fit.cpu().numpy(), trd.cpu().numpy()
+    for i, ep in enumerate(eps):
+        f, t = _oracle_eval(oracle, ep)
+        assert trd[i] == t and fit[i] == f, (lens[i], fit[i], f)
+    assert fit[0] == -50.0 and trd[0] == 0  # empty episode: idle penalty only
+
+
+def test_nan_bounds_and_h32_long(sgmm, oracle):
+    eps = _synthetic_batch(sgmm, 6, 3600, 32, seed=21, nan_frac=0.03)
+    (fit, trd), _ = _run_batch(sgmm, eps, False)
+    for i, ep in enumerate(eps):
+        f, t = _oracle_eval(oracle, ep)
+        assert trd[i].item() == t and fit[i].item() == f
+
+
+def test_bench_config_population(sgmm, oracle):
+    """BASELINE config 2 shape (P=64, H=16, T=3600): every episode bit-exact."""
+    from sgmm_amd import synthetic
+    P, T, H = 64, 3600, 16
+    b = synthetic.bundle_510300(T, seed=0)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=0.05, seed=1)
+    fit, trd = sgmm.evaluate_population(pop, None, b, 0.0001, 0.001, 0.0, st)
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    ticks = (s1n, s2n) + tuple(b[2:])
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, ticks, np.arange(P), None,
+                                           np.zeros(P), np.full(P, T), np.zeros(P),
+                                           [oracle.params(phi=0.0001, tick=0.001)], n_threads=8)
+    assert np.array_equal(trd, want_t)
+    assert np.array_equal(fit, want_f)
+
+
+def test_inventory_range_variants(sgmm, oracle):
+    """Non-default caps (i_max=1, i_min=-3): 5 states, 0 not centred."""
+    eps = _synthetic_batch(sgmm, 4, 700, 16, seed=31, sigma=0.5)
+    ticks = sgmm.TickStore()
+    segs = [ticks.add((e["s1"], e["s2"], e["mid"], e["ask"], e["bid"], e["buy_max"], e["sell_min"]),
+                      e["train_stats"]) for e in eps]
+    ticks.to(DEV)
+    cfg = sgmm.EnvConfig(phi=0.002, tick_size=0.001, i_max=1, i_min=-3)
+    params = sgmm.params_tensor([cfg], DEV)
+    mm = torch.from_numpy(np.stack([e["mm"] for e in eps])).to(DEV)
+    eb = sgmm.EpisodeBatch(np.arange(4), [ticks.segments[s][0] for s in segs], [700] * 4, np.zeros(4),
+                           inv_min=-3, inv_max=1).to(DEV)
+    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, mm, 16)
+    for i, ep in enumerate(eps):
+        p = oracle.params(phi=0.002, tick=0.001, i_max=1, i_min=-3)
+        f, t = oracle.evaluate(ep["mm"], 16, None, ep["s1n"], ep["s2n"], ep["mid"], ep["ask"], ep["bid"],
+                               ep["buy_max"], ep["sell_min"], p)
+        assert trd[i].item() == t and fit[i].item() == f
+
+
+def test_dropin_evaluate_individual(golden, sgmm):
+    """The reference-signature entry point reproduces the reference's own fitness."""
+    d = golden("g2_synthetic.npz")
+    for ep in list(episodes_from_fixture(d))[:8]:
+        st = stats_dict(ep["stats"], ep["stats_nb"])
+        bundle = (ep["s1"], ep["s2"], ep["mid"], ep["ask"], ep["bid"], ep["buy_max"], ep["sell_min"])
+        f, t = sgmm.evaluate_individual(torch.from_numpy(ep["mm"]), None if ep["adv"] is None else
+                                        torch.from_numpy(ep["adv"]), bundle, ep["phi"], ep["tick"],
+                                        ep["fee"], st, use_arl=ep["adv"] is not None)
+        assert f == ep["fitness"] and t == ep["trades"]
