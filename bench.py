@@ -1,0 +1,256 @@
+#!/usr/bin/env python
+"""Benchmark: env-steps/sec of the GA population rollout (BASELINE.json metric).
+
+One step = one GA generation of BASELINE config 2 on every GPU:
+  ask (population from master + sigma * N(0,1), on device)
+  -> rollout of the population's training episodes (+ fused validation
+     episodes of the same genomes) through sgmm_rollout_fitness
+  -> [N > 1: RCCL all-gather of fitness]
+  -> tell (argmax, new master) -> validation bookkeeping / sigma decay.
+Workload per GPU: population 64, TradingPolicy 3->16->16->2 (H=16), synthetic
+510300.SH-shaped ticks, 3600 training ticks + 720 validation ticks, phi=1e-4,
+tick 0.001, no adversary.  Weak scaling: each rank owns 64 individuals of a
+64*N population.  value = N * 64 * 3600 training env-steps per generation /
+measured seconds per generation (validation ticks are not counted).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) runs BEFORE
+the GPU is touched: the reference-equivalent batch-1 torch loop
+(oracle/ref_loop.py) under a fork Pool, on one generation of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "env-steps/sec (pop×ticks) at 1/2/4/8 MI355X; generations/sec vs CPU ref"
+FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
+HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md: HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--pop", type=int, default=64, help="population per GPU")
+    ap.add_argument("--hidden", type=int, default=16)
+    ap.add_argument("--ticks", type=int, default=3600)
+    ap.add_argument("--val-ticks", type=int, default=720)
+    ap.add_argument("--phi", type=float, default=0.0001)
+    ap.add_argument("--profile-steps", type=int, default=20,
+                    help="eager generations timed kernel by kernel with HIP events")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, cpu_count)")
+    ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest in profiles/)")
+    return ap.parse_args()
+
+
+def flop_per_step(H: int) -> int:
+    """Algorithmic FLOP of one env-step's policy forward: 2 * (3H + H*H + 2H)."""
+    return 2 * (3 * H + H * H + 2 * H)
+
+
+def workload(args, seed=0):
+    import sgmm_pkg
+    sgmm_pkg.load()
+    from sgmm_amd import synthetic
+    train = synthetic.bundle_510300(args.ticks, seed=seed)
+    val = synthetic.bundle_510300(args.val_ticks, seed=seed + 1, start_ticks=3500)
+    return train, val, synthetic.train_stats(train)
+
+
+def cpu_baseline(args):
+    """Reference-equivalent CPU loop on one generation of the workload (before any GPU use)."""
+    import numpy as np
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    import ref_loop
+    import sgmm_pkg
+    sgmm_pkg.load()
+    from sgmm_amd import synthetic
+    train, _, stats = workload(args)
+    pop = synthetic.population(args.pop, args.hidden, sigma=0.05, seed=7).numpy()
+    workers = args.cpu_workers or min(16, os.cpu_count() or 1)
+    fit, trd, dt, workers = ref_loop.population(pop, None, train, args.phi, 0.001, 0.0, stats,
+                                                args.hidden, workers=workers)
+    steps = args.pop * args.ticks
+    # the C restatement as a "best CPU" line (same sample, OpenMP threads)
+    s1n, s2n = oracle.normalize_signals(train[0], train[1], stats)
+    ticks = (s1n, s2n) + tuple(train[2:])
+    t0 = time.perf_counter()
+    cf, ct = oracle.evaluate_batch(pop, args.hidden, None, ticks, np.arange(args.pop), None,
+                                   np.zeros(args.pop), np.full(args.pop, args.ticks), np.zeros(args.pop),
+                                   [oracle.params(phi=args.phi, tick=0.001)], n_threads=workers)
+    dtc = time.perf_counter() - t0
+    same = bool(np.array_equal(np.array(trd), ct))
+    try:
+        cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        cpu_model = "unknown"
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": (f"one generation of the bench workload ({args.pop} episodes x {args.ticks} ticks, "
+                       f"H={args.hidden}) through oracle/ref_loop.py (reference batch-1 torch loop "
+                       f"restated) on a fork Pool of {workers} workers, torch threads=1"),
+            "seconds": dt, "cpu_model": cpu_model,
+            "c_oracle": {"value": steps / dtc, "cores": workers, "seconds": dtc,
+                         "trades_agree_with_port": same}}
+
+
+def latest_pmc(path_arg):
+    if path_arg:
+        p = Path(path_arg)
+    else:
+        cands = sorted((ROOT / "profiles").glob("*pmc_traffic*.json"))
+        if not cands:
+            return None
+        p = cands[-1]
+    try:
+        return json.loads(p.read_text()) | {"file": str(p.relative_to(ROOT)) if p.is_absolute() else str(p)}
+    except Exception:
+        return None
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args)  # before the GPU is initialised (fork Pool)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    import sgmm_pkg
+    sgmm = sgmm_pkg.load()
+    from sgmm_amd import _lib
+
+    train, val, stats = workload(args)
+    P, H, T = args.pop, args.hidden, args.ticks
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    tmp = tempfile.mkdtemp(prefix="sgmm_bench_")
+    eng = sgmm.DRLEngine(pop_size=P * world, phi=args.phi, tick_size=0.001, fee_rate=0.0,
+                         use_arl=False, save_dir=tmp, hidden_dim=H, rng="device", seed=1234,
+                         val_mode="fused", sync_every=10**9, verbose=False,
+                         use_graph=not args.no_graph)
+    sess = eng.session(train, val, stats, generations=args.warmup + args.steps)
+    for g in range(args.warmup):
+        sess.step(g)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for g in range(args.warmup, args.warmup + args.steps):
+        sess.step(g)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    _, hist = sess.finish()
+    ms_per_step = dt / args.steps * 1e3
+    value = world * P * T * args.steps / dt
+
+    # per-kernel durations: eager generations of the same workload bracketed by
+    # HIP events on the launch stream (sgmm_profile_*); graph replays launch the
+    # identical kernels
+    peng = sgmm.DRLEngine(pop_size=P, phi=args.phi, tick_size=0.001, use_arl=False, save_dir=tmp,
+                          hidden_dim=H, rng="device", seed=99, val_mode="fused", sync_every=10**9,
+                          verbose=False, use_graph=False, dist=False)
+    psess = peng.session(train, val, stats, generations=args.profile_steps + 2)
+    psess.step(0)
+    psess.step(1)
+    torch.cuda.synchronize()
+    _lib.profile_read()
+    _lib.profile_enable(True)
+    for g in range(2, 2 + args.profile_steps):
+        psess.step(g)
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    prof = _lib.profile_read()
+    psess.finish()
+    kernels = {k: {"avg_us": 1e3 * v[0] / v[1], "launches": v[1]} for k, v in prof.items()}
+    gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, args.profile_steps)
+
+    # roofline of the policy-table kernel (the FP32 compute kernel of the path)
+    steps_per_launch = P * (T + args.val_ticks)  # fused validation: train + val episodes
+    fl = flop_per_step(H)
+    tab = kernels.get("policy_table")
+    pmc = latest_pmc(args.pmc)
+    roofline = None
+    if tab:
+        achieved = steps_per_launch * fl / (tab["avg_us"] * 1e-6) / 1e12
+        traffic = None
+        if pmc and pmc.get("kernels", {}).get("policy_table"):
+            traffic = pmc["kernels"]["policy_table"].get("hbm_bytes_per_launch")
+        roofline = {"bound": "mfma", "pipe": "fp32 VALU (gfx950 f32 MFMA peak == f32 VALU peak)",
+                    "kernel": "k_policy_table", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+                    "algorithmic": {"flop_per_env_step": fl,
+                                    "env_steps_per_launch": steps_per_launch,
+                                    "note": "algorithmic = one policy forward per env-step; the table "
+                                            "kernel evaluates all 5 inventory states (5x this work)"},
+                    "avg_launch_us": tab["avg_us"]}
+        if traffic:
+            gbps = traffic / (tab["avg_us"] * 1e-6) / 1e9
+            roofline["hbm"] = {"achieved_GBps": gbps, "peak_GBps": HBM_PEAK_GBPS,
+                               "frac": gbps / HBM_PEAK_GBPS, "source": pmc.get("file")}
+    dominant = max(kernels.items(), key=lambda kv: kv[1]["avg_us"] * kv[1]["launches"])[0] if kernels else None
+
+    if rank == 0:
+        gens_per_s = args.steps / dt
+        out = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32+f64", "data": "synthetic",
+            "config": {"workload": "BASELINE config 2: GA generation, population 64/GPU, "
+                                   "TradingPolicy 3->16->16->2, synthetic 510300.SH ticks "
+                                   f"({T} train + {args.val_ticks} fused validation), no adversary",
+                       "population_per_gpu": P, "global_population": P * world, "hidden": H,
+                       "ticks_train": T, "ticks_val": args.val_ticks, "phi": args.phi,
+                       "parallelism": f"population shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
+                       "hip_graph": bool(sess.use_graph)},
+            "generations_per_s": gens_per_s,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu else None,
+            "kernels": kernels,
+            "dominant_kernel": dominant,
+            "gen_kernel_time_us": gen_kernel_us,
+            "final_train_f": float(hist["train_f"][-1]) if hist["train_f"] else None,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -83,11 +83,15 @@ SIGNATURES = {
                                             _VP, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _SZ, _VP]),
     "sgmm_rollout_trace": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
                                           _VP, _I64, _I32, _VP, _I64] + [_VP] * 16),
-    "sgmm_ga_ask": (ctypes.c_int, [_VP, _I64, _VP, _U64, _U32, _U32, _I32, _I32, _VP, _I64, _VP]),
+    "sgmm_ga_ask": (ctypes.c_int, [_VP, _I64, _VP, _U32, _U64, _I32, _I32, _VP, _I64, _VP]),
     "sgmm_ga_state_init": (ctypes.c_int, [_VP, _D, _I32, _D, _VP]),
     "sgmm_ga_tell": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _VP, _I64, _I64,
-                                    _I64, _U64, _U32, _VP, _VP]),
-    "sgmm_ga_val_update": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _VP]),
+                                    _I64, _U64, _VP, _I32, _VP]),
+    "sgmm_ga_val_update": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _I32, _VP]),
+    "sgmm_ga_step": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _I32, _VP, _VP, _VP, _I64, _I64, _U64,
+                                    _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
+    "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),
+    "sgmm_profile_read": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
 }
 
 _lib = None
@@ -136,3 +140,21 @@ def require_gpu():
     if not torch.cuda.is_available():
         raise SgmmError("no HIP device visible: the sgmm rollout path runs only on the GPU "
                         "(MI355X / gfx950); there is no CPU fallback")
+
+
+def profile_enable(on: bool = True):
+    load().sgmm_profile_enable(1 if on else 0)
+
+
+def profile_read(max_kinds: int = 32) -> dict:
+    """{kernel kind: (total_ms, launches)} since the last read (waits for events)."""
+    import numpy as np
+    L = load()
+    names = ctypes.create_string_buffer(48 * max_kinds)
+    tot = np.zeros(max_kinds, np.float64)
+    cnt = np.zeros(max_kinds, np.int64)
+    n = L.sgmm_profile_read(max_kinds, names, tot.ctypes.data, cnt.ctypes.data)
+    check(n if n < 0 else 0, "sgmm_profile_read")
+    raw = names.raw
+    return {raw[48 * i:48 * i + 48].split(b"\0", 1)[0].decode(): (float(tot[i]), int(cnt[i]))
+            for i in range(n)}

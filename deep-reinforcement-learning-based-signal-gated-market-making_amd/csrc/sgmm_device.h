@@ -19,7 +19,14 @@ namespace sgmm {
 
 constexpr int kWave = 64;
 
-__device__ __forceinline__ float relu(float a) { return a < 0.0f ? 0.0f : a; }
+// ReLU on the float's bit pattern: max(bits, 0) as a signed integer (one
+// v_max_i32, no NaN canonicalisation).  Equals torch's relu for every
+// non-NaN input (-0.0 -> +0.0); a NaN keeps its payload if positive and becomes
+// 0 if negative -- NaN only arises from NaN state inputs, where the
+// reference's own action cast (NaN -> int) is undefined anyway.
+__device__ __forceinline__ float relu(float a) {
+    return __int_as_float(max(__float_as_int(a), 0));
+}
 
 // float -> int action: saturating, NaN -> INT32_MIN (the x86 cvtt value numpy's
 // astype(int) produces).  Values are already integral (rint) when called.

@@ -30,16 +30,16 @@ __device__ __forceinline__ void ask_row4(const float* __restrict__ master, int64
 }
 
 __global__ void k_ga_ask(const float* __restrict__ master, int64_t n_params,
-                         const double* __restrict__ sigma, uint64_t seed, uint32_t sid,
-                         uint32_t gen, int32_t i0, int32_t n, float* __restrict__ out,
-                         int64_t out_stride) {
+                         const sgmm_ga_state* __restrict__ st, uint32_t sid, uint64_t seed,
+                         int32_t i0, int32_t n, float* __restrict__ out, int64_t out_stride) {
     const int64_t nk4 = (n_params + 3) / 4;
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= nk4 * n) return;
     const int32_t i = (int32_t)(g / nk4);
     const int64_t k4 = g - (int64_t)i * nk4;
+    const float sig = (float)(sid == 0 ? st->sigma_mm : st->sigma_adv);
     float v[4];
-    ask_row4(master, n_params, (float)*sigma, seed, sid, gen, (uint32_t)(i0 + i), k4, v);
+    ask_row4(master, n_params, sig, seed, sid, (uint32_t)st->gen, (uint32_t)(i0 + i), k4, v);
     float* row = out + (int64_t)i * out_stride;
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -62,8 +62,10 @@ __global__ __launch_bounds__(kTellBlock) void k_ga_tell(
     const int32_t* __restrict__ trades, int32_t P, float* __restrict__ master_mm,
     const float* __restrict__ pop_mm, int64_t pop_mm_stride, float* __restrict__ master_adv,
     const float* __restrict__ pop_adv, int64_t pop_adv_stride, int64_t n_mm, int64_t n_adv,
-    uint64_t seed, uint32_t gen, sgmm_ga_history* __restrict__ hist) {
+    uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap) {
     __shared__ double sv[2][kTellBlock];
+    const uint32_t gen = (uint32_t)st->gen;
+    sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
     __shared__ int si[2][kTellBlock];
     const int tid = threadIdx.x;
     double bv = 0.0, av = 0.0;
@@ -135,8 +137,10 @@ __global__ __launch_bounds__(kTellBlock) void k_ga_tell(
 __global__ __launch_bounds__(kTellBlock) void k_ga_val_update(
     sgmm_ga_state* __restrict__ st, const double* __restrict__ vfit,
     const int32_t* __restrict__ vtrades, int32_t use_best, const float* __restrict__ master,
-    float* __restrict__ best_master, int64_t n, sgmm_ga_history* __restrict__ hist) {
+    float* __restrict__ best_master, int64_t n, sgmm_ga_history* __restrict__ history,
+    int32_t hist_cap) {
     __shared__ int improved;
+    sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
     const int idx = use_best ? st->best_idx : 0;
     const double v = vfit[idx];
     if (threadIdx.x == 0) improved = v > st->best_val;  // drl_engine.py:143 (NaN -> False)
@@ -187,21 +191,173 @@ __global__ void k_ga_state_init(sgmm_ga_state* st, double sigma, int32_t patienc
     st->decay = decay;
 }
 
+// ---------------------------------------------------------------- fused boundary
+constexpr int kStepBlock = 1024;
+constexpr int kMaxStepParams = 4096;  // master staged in LDS
+
+__device__ void block_argmax2(const double* __restrict__ fit, int P, int& best, int& abest,
+                              double* sv, int* si) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    double bv = 0.0, av = 0.0;
+    int bi = -1, aj = -1;
+    for (int i = tid; i < P; i += nt) {
+        const double f = fit[i];
+        if (bi < 0 || better(f, i, bv, bi)) { bv = f; bi = i; }
+        if (aj < 0 || better(-f, i, av, aj)) { av = -f; aj = i; }
+    }
+    sv[tid] = bv; si[tid] = bi;
+    sv[nt + tid] = av; si[nt + tid] = aj;
+    __syncthreads();
+    for (int w = nt / 2; w > 0; w >>= 1) {
+        if (tid < w) {
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                const int o = r * nt;
+                const int io = si[o + tid + w];
+                if (io >= 0 && (si[o + tid] < 0 || better(sv[o + tid + w], io, sv[o + tid], si[o + tid]))) {
+                    sv[o + tid] = sv[o + tid + w];
+                    si[o + tid] = io;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    best = si[0];
+    abest = si[nt];
+}
+
+// master <- ask(best) in place; staged copy to LDS for the next ask
+__device__ void regen_master(float* __restrict__ master, float* lds_master, int64_t n, float sig,
+                             uint64_t seed, uint32_t sid, uint32_t gen, int best) {
+    for (int64_t k4 = threadIdx.x; k4 < (n + 3) / 4; k4 += blockDim.x) {
+        float v[4];
+        ask_row4(master, n, sig, seed, sid, gen, (uint32_t)best, k4, v);
+        for (int q = 0; q < 4; ++q)
+            if (4 * k4 + q < n) {
+                master[4 * k4 + q] = v[q];
+                lds_master[4 * k4 + q] = v[q];
+            }
+    }
+}
+
+__device__ void ask_rows(const float* lds_master, int64_t n, float sig, uint64_t seed,
+                         uint32_t sid, uint32_t gen, int32_t i0, int32_t cnt,
+                         float* __restrict__ out) {
+    const int64_t nk4 = (n + 3) / 4;
+    for (int64_t g = threadIdx.x; g < nk4 * cnt; g += blockDim.x) {
+        const int32_t i = (int32_t)(g / nk4);
+        const int64_t k4 = g - (int64_t)i * nk4;
+        float v[4];
+        ask_row4(lds_master, n, sig, seed, sid, gen, (uint32_t)(i0 + i), k4, v);
+        for (int q = 0; q < 4; ++q)
+            if (4 * k4 + q < n) out[(int64_t)i * n + 4 * k4 + q] = v[q];
+    }
+}
+
+__global__ __launch_bounds__(kStepBlock) void k_ga_step(
+    sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
+    const int32_t* __restrict__ trades, const double* __restrict__ vfit,
+    const int32_t* __restrict__ vtrades, int32_t P, float* __restrict__ master,
+    float* __restrict__ master_adv, float* __restrict__ best_master, int64_t n_mm, int64_t n_adv,
+    uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap,
+    float* __restrict__ next_mm, float* __restrict__ next_adv, int32_t i0, int32_t n) {
+    __shared__ double sv[2 * kStepBlock];
+    __shared__ int si[2 * kStepBlock];
+    __shared__ float lm[kMaxStepParams];
+    __shared__ float la[kMaxStepParams];
+    __shared__ int improved;
+    __shared__ float next_sig[2];
+    const int tid = threadIdx.x;
+    const uint32_t gen = (uint32_t)st->gen;
+    sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
+    int best, abest;
+    block_argmax2(fit, P, best, abest, sv, si);
+    const float sig_mm = (float)st->sigma_mm, sig_adv = (float)st->sigma_adv;
+    __syncthreads();
+    // tell (model.py:73-76; drl_engine.py:119-125)
+    regen_master(master, lm, n_mm, sig_mm, seed, 0u, gen, best);
+    if (master_adv) regen_master(master_adv, la, n_adv, sig_adv, seed, 1u, gen, abest);
+    if (tid == 0) {
+        // validation of the best (drl_engine.py:129-171)
+        const double v = vfit[best];
+        improved = v > st->best_val;
+        int decayed = 0;
+        if (improved) {
+            st->best_val = v;
+            st->no_improve = 0;
+        } else {
+            st->no_improve += 1;
+        }
+        if (st->no_improve >= st->patience) {
+            st->sigma_mm *= st->decay;
+            st->sigma_adv *= st->decay;
+            st->no_improve = 0;
+            decayed = 1;
+        }
+        st->best_idx = best;
+        st->adv_best_idx = abest;
+        st->last_train_f = fit[best];
+        st->improved = improved;
+        st->decayed = decayed;
+        st->last_val_f = v;
+        st->gen += 1;
+        next_sig[0] = (float)st->sigma_mm;
+        next_sig[1] = (float)st->sigma_adv;
+        if (hist) {
+            hist->train_f = fit[best];
+            hist->train_trades = trades ? trades[best] : 0;
+            hist->best_idx = best;
+            hist->val_f = v;
+            hist->val_trades = vtrades ? vtrades[best] : 0;
+            hist->sigma_after = st->sigma_mm;
+            hist->flags = improved | (decayed << 1);
+        }
+    }
+    __syncthreads();
+    if (improved && best_master)
+        for (int64_t k = tid; k < n_mm; k += kStepBlock) best_master[k] = lm[k];
+    // ask of the next generation (model.py:65-71) from the new master / sigma
+    if (next_mm) ask_rows(lm, n_mm, next_sig[0], seed, 0u, gen + 1, i0, n, next_mm);
+    if (next_adv && master_adv) ask_rows(la, n_adv, next_sig[1], seed, 1u, gen + 1, i0, n, next_adv);
+}
+
 }  // namespace sgmm
 
 using namespace sgmm;
 
-extern "C" int sgmm_ga_ask(const float* master, int64_t n_params, const double* sigma,
-                           uint64_t seed, uint32_t stream_id, uint32_t gen, int32_t i0, int32_t n,
-                           float* out, int64_t out_stride, void* stream) {
+extern "C" int sgmm_ga_step(sgmm_ga_state* state, const double* fitness, const int32_t* trades,
+                            const double* val_fitness, const int32_t* val_trades, int32_t P,
+                            float* master_mm, float* master_adv, float* best_master,
+                            int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
+                            sgmm_ga_history* history, int32_t history_cap, float* next_pop_mm,
+                            float* next_pop_adv, int32_t i0, int32_t n, void* stream) {
     clear_error();
-    SGMM_REQUIRE(master && sigma && out, "null pointer");
+    SGMM_REQUIRE(state && fitness && val_fitness && master_mm, "null pointer");
+    SGMM_REQUIRE(P > 0 && n_params_mm > 0 && n_params_mm <= kMaxStepParams, "bad P / n_params_mm");
+    SGMM_REQUIRE(!master_adv || (n_params_adv > 0 && n_params_adv <= kMaxStepParams), "n_params_adv");
+    SGMM_REQUIRE(!next_pop_mm || (n >= 0 && i0 >= 0), "bad next-ask shard");
+    ProfScope prof("ga_step", as_stream(stream));
+    hipLaunchKernelGGL(k_ga_step, dim3(1), dim3(kStepBlock), 0, as_stream(stream), state,
+                       fitness, trades, val_fitness, val_trades, P, master_mm, master_adv,
+                       best_master, n_params_mm, n_params_adv, seed, history, history_cap,
+                       next_pop_mm, next_pop_adv, i0, n);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_ga_ask(const float* master, int64_t n_params, const sgmm_ga_state* state,
+                           uint32_t stream_id, uint64_t seed, int32_t i0, int32_t n, float* out,
+                           int64_t out_stride, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(master && state && out, "null pointer");
+    SGMM_REQUIRE(stream_id <= 1, "stream_id must be 0 (mm) or 1 (adversary)");
     SGMM_REQUIRE(n_params > 0 && n >= 0 && i0 >= 0 && out_stride >= n_params, "bad shape");
     if (n == 0) return SGMM_OK;
     const int64_t work = ((n_params + 3) / 4) * (int64_t)n;
+    ProfScope prof("ga_ask", as_stream(stream));
     hipLaunchKernelGGL(k_ga_ask, dim3((unsigned)((work + 255) / 256)), dim3(256), 0,
-                       as_stream(stream), master, n_params, sigma, seed, stream_id, gen, i0, n,
-                       out, out_stride);
+                       as_stream(stream), master, n_params, state, stream_id, seed, i0, n, out,
+                       out_stride);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }
@@ -220,7 +376,7 @@ extern "C" int sgmm_ga_tell(sgmm_ga_state* state, const double* fitness, const i
                             int32_t P, float* master_mm, const float* pop_mm,
                             int64_t pop_mm_stride, float* master_adv, const float* pop_adv,
                             int64_t pop_adv_stride, int64_t n_params_mm, int64_t n_params_adv,
-                            uint64_t seed, uint32_t gen, sgmm_ga_history* history_row,
+                            uint64_t seed, sgmm_ga_history* history, int32_t history_cap,
                             void* stream) {
     clear_error();
     SGMM_REQUIRE(state && fitness && master_mm, "null pointer");
@@ -228,9 +384,10 @@ extern "C" int sgmm_ga_tell(sgmm_ga_state* state, const double* fitness, const i
     SGMM_REQUIRE(!pop_mm || pop_mm_stride >= n_params_mm, "pop_mm_stride too small");
     SGMM_REQUIRE(!master_adv || n_params_adv > 0, "n_params_adv");
     SGMM_REQUIRE(!pop_adv || pop_adv_stride >= n_params_adv, "pop_adv_stride too small");
+    ProfScope prof("ga_tell", as_stream(stream));
     hipLaunchKernelGGL(k_ga_tell, dim3(1), dim3(kTellBlock), 0, as_stream(stream), state,
                        fitness, trades, P, master_mm, pop_mm, pop_mm_stride, master_adv, pop_adv,
-                       pop_adv_stride, n_params_mm, n_params_adv, seed, gen, history_row);
+                       pop_adv_stride, n_params_mm, n_params_adv, seed, history, history_cap);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }
@@ -238,13 +395,14 @@ extern "C" int sgmm_ga_tell(sgmm_ga_state* state, const double* fitness, const i
 extern "C" int sgmm_ga_val_update(sgmm_ga_state* state, const double* val_fitness,
                                   const int32_t* val_trades, int32_t use_best_index,
                                   const float* master_mm, float* best_master, int64_t n_params_mm,
-                                  sgmm_ga_history* history_row, void* stream) {
+                                  sgmm_ga_history* history, int32_t history_cap, void* stream) {
     clear_error();
     SGMM_REQUIRE(state && val_fitness && master_mm, "null pointer");
     SGMM_REQUIRE(n_params_mm > 0, "n_params_mm");
+    ProfScope prof("ga_val_update", as_stream(stream));
     hipLaunchKernelGGL(k_ga_val_update, dim3(1), dim3(kTellBlock), 0, as_stream(stream), state,
                        val_fitness, val_trades, use_best_index, master_mm, best_master,
-                       n_params_mm, history_row);
+                       n_params_mm, history, history_cap);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }

@@ -42,6 +42,18 @@ void clear_error();
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Kernel-timing hooks (sgmm_profile_enable).  prof_begin returns a slot
+// (or -1 when profiling is off) that prof_end closes on the same stream.
+int prof_begin(const char* kind, hipStream_t s);
+void prof_end(int slot, hipStream_t s);
+
+struct ProfScope {
+    int slot;
+    hipStream_t s;
+    ProfScope(const char* kind, hipStream_t st) : slot(prof_begin(kind, st)), s(st) {}
+    ~ProfScope() { prof_end(slot, s); }
+};
+
 inline bool supported_hidden(int h) { return h == 8 || h == 16 || h == 32 || h == 64; }
 
 }  // namespace sgmm

@@ -27,12 +27,14 @@
 // Trace path (sgmm_rollout_trace): k_rollout_direct, one wave per episode,
 // lane = hidden neuron, the literal step loop (independent second
 // implementation; the tests require both paths to agree bit for bit).
+#include <cstdlib>
+#include <cstring>
+
 #include "sgmm_device.h"
 #include "sgmm_internal.h"
 
 namespace sgmm {
 
-constexpr int kTableBlock = 256;
 constexpr int kChunk = 64;          // ticks per chunk in the path scan
 constexpr int kSeg = 4096;          // ticks summed per LDS segment
 constexpr int kScanBlock = 256;
@@ -47,29 +49,79 @@ struct EpArrays {
     const int32_t* param;
 };
 
-__device__ __forceinline__ int next_state(int s, int code, bool arl) {
-    const int fb = code & 1, fs = code >> 1;
-    if (!arl) return s + fb - fs;
-    return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
+// ------------------------------------------------------------------ transition maps
+// A step's effect on the (<= 8) inventory states is a map state -> state,
+// packed 3 bits per state in a u32 (bits 0..23).  Composition is cheap VALU
+// work, so a wave of 64 ticks builds the exclusive prefix of its chunk with
+// log2(64) shuffle rounds and the scan kernel reads every tick's state with
+// one field lookup.
+constexpr uint32_t kIdentityMap = 0xFAC688u;  // x -> x for x = 0..7
+
+__device__ __forceinline__ uint32_t map_get(uint32_t m, uint32_t x) { return (m >> (3u * x)) & 7u; }
+
+// "first a, then b" on the first NSM states
+template <int NSM>
+__device__ __forceinline__ uint32_t map_then(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int x = 0; x < NSM; ++x) r |= map_get(b, map_get(a, x)) << (3 * x);
+    return r;
+}
+
+__device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
+    // chunk-map slot of episode e: regions of ceil(len/64) never overlap
+    return (uint32_t)((step_off + (int64_t)kChunk * e) / kChunk);
 }
 
 // ------------------------------------------------------------------ table
-template <int H, bool ARL>
-__global__ __launch_bounds__(kTableBlock) void k_policy_table(
+// Block = 64 consecutive ticks of one episode x nsi inventory states: wave w
+// evaluates the policy and the FPT step for every tick of the block from
+// inventory inv_min + w (one lane per (tick, state)).  The genome is
+// wave-uniform, so weights arrive by scalar loads straight into the FMAs'
+// SGPR operands, each used once (no loop-invariant hoisting, no SGPR spills,
+// ~H+16 VGPRs -> full occupancy).  The 64-tick slice of the tick stream is
+// staged once in LDS (coalesced) and read by all waves.  Wave 0 then turns the
+// per-state fills into the chunk's transition maps.  Outputs per tick:
+//   !ARL: words[row] = exclusive prefix map of the tick within its 64-tick
+//         chunk | traded-mask << 24; cmaps[chunk] = the chunk's full map;
+//    ARL: fills[row] = 2 fill bits per (inventory, sell flag, buy flag) state;
+// and rew[row * ns + state] = the step reward from that state (float64).
+template <int H, int NSM, bool ARL>
+__global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
     const float* __restrict__ mm, int64_t mm_stride, const float* __restrict__ adv,
-    int64_t adv_stride, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ fills,
-    double* __restrict__ rew) {
-    using L = GenomeLayout<H>;
+    int64_t adv_stride, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
-    const int32_t t0 = blockIdx.x * kTableBlock;
+    const int32_t t0 = blockIdx.x * kChunk;
     if (t0 >= T) return;  // block-uniform
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const int ns = ARL ? 4 * nsi : nsi;
     const sgmm_env_params p = params[ep.param[e]];
     const float* __restrict__ g = mm + (int64_t)ep.genome[e] * mm_stride;
 
-    __shared__ int32_t lut[2][32];  // adversary (delta_a, delta_b) per state
+    __shared__ float sx[2][kChunk];
+    __shared__ double spx[5][kChunk];
+    __shared__ uint8_t code[32][kChunk];
+    __shared__ int32_t lut[2][32];
+    // stage the tick slice: column c by wave c % nsi
+    const int64_t tbase = ep.tick_off[e] + t0;
+    const int nvalid = min(kChunk, T - t0);
+    for (int c = w; c < 7; c += nsi) {
+        if (lane < nvalid) {
+            const int64_t ti = tbase + lane;
+            switch (c) {
+                case 0: sx[0][lane] = tk.s1n[ti]; break;
+                case 1: sx[1][lane] = tk.s2n[ti]; break;
+                case 2: spx[0][lane] = tk.mid_next[ti]; break;
+                case 3: spx[1][lane] = tk.best_ask[ti]; break;
+                case 4: spx[2][lane] = tk.best_bid[ti]; break;
+                case 5: spx[3][lane] = tk.buy_max[ti]; break;
+                default: spx[4][lane] = tk.sell_min[ti]; break;
+            }
+        }
+    }
     if (ARL) {
         const int ai = ep.adv ? ep.adv[e] : -1;
         if ((int)threadIdx.x < ns) {
@@ -81,67 +133,442 @@ __global__ __launch_bounds__(kTableBlock) void k_policy_table(
             lut[0][s] = da;
             lut[1][s] = db;
         }
-        __syncthreads();
     }
-    const int32_t t = t0 + threadIdx.x;
-    if (t >= T) return;
-
-    const int64_t ti = ep.tick_off[e] + t;
-    const float x0 = tk.s1n[ti], x1 = tk.s2n[ti];
-    const double mid = tk.mid_next[ti], ask = tk.best_ask[ti], bid = tk.best_bid[ti];
-    const double bmax = tk.buy_max[ti], smin = tk.sell_min[ti];
-
-    // tick-dependent part of layer 1 (shared by every inventory state):
-    // acc = b1; acc = fma(W1[j,0], s1n, acc); acc = fma(W1[j,1], s2n, acc)
-    float pre[H];
-#pragma unroll
-    for (int j = 0; j < H; ++j)
-        pre[j] = __builtin_fmaf(g[L::W1 + 3 * j + 1], x1,
-                                __builtin_fmaf(g[L::W1 + 3 * j], x0, g[L::B1 + j]));
-
-    const int64_t row = ep.step_off[e] + t;
-    double* __restrict__ R = rew + row * ns;
-    uint64_t fw = 0;
-    for (int si = 0; si < nsi; ++si) {
-        const int32_t inv = inv_min + si;
-        const float x2 = (float)((double)inv / 2.0);  // drl_engine.py:35
-        float h1[H];
-#pragma unroll
-        for (int j = 0; j < H; ++j) h1[j] = relu(__builtin_fmaf(g[L::W1 + 3 * j + 2], x2, pre[j]));
-        float o0 = g[L::B3], o1 = g[L::B3 + 1];
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-            float a = g[L::B2 + j];
-#pragma unroll
-            for (int k = 0; k < H; ++k) a = __builtin_fmaf(g[L::W2 + j * H + k], h1[k], a);
-            const float h2 = relu(a);
-            o0 = __builtin_fmaf(g[L::W3 + j], h2, o0);
-            o1 = __builtin_fmaf(g[L::W3 + H + j], h2, o1);
-        }
+    __syncthreads();
+    const bool valid = lane < nvalid;
+    if (valid) {
+        const int32_t inv = inv_min + w;
+        float o0, o1;
+        mlp_forward<H>(g, sx[0][lane], sx[1][lane], (float)((double)inv / 2.0), o0, o1);
         const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
         const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+        const double mid = spx[0][lane], ask = spx[1][lane], bid = spx[2][lane];
+        const double bmax = spx[3][lane], smin = spx[4][lane];
+        double* __restrict__ R = rew + (ep.step_off[e] + t0 + lane) * ns;
         if (!ARL) {
             const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
-            fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * si);
-            R[si] = so.reward;
+            code[w][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
+            R[w] = so.reward;
         } else {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int s = 4 * si + q;
-                const StepOut so = ftp_step(p, inv, oa + lut[0][s], ob + lut[1][s], mid, ask, bid,
-                                            bmax, smin);
-                fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * s);
+            for (int c = 0; c < 4; ++c) {
+                const int s = 4 * w + c;
+                const StepOut so = ftp_step(p, inv, oa + lut[0][s], ob + lut[1][s], mid, ask,
+                                            bid, bmax, smin);
+                code[s][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
                 R[s] = so.reward;
             }
         }
     }
-    fills[row] = fw;
+    __syncthreads();
+    if (w != 0) return;
+    const int64_t row = ep.step_off[e] + t0 + lane;
+    if (ARL) {
+        if (valid) {
+            uint64_t fw = 0;
+            for (int s = 0; s < ns; ++s) fw |= (uint64_t)code[s][lane] << (2 * s);
+            fills[row] = fw;
+        }
+        return;
+    }
+    uint32_t map = kIdentityMap, traded = 0;
+    if (valid) {
+        map = 0;
+        for (int s = 0; s < nsi; ++s) {
+            const uint32_t c = code[s][lane];
+            map |= (uint32_t)(s + (int)(c & 1u) - (int)(c >> 1)) << (3 * s);
+            traded |= (uint32_t)(c != 0) << s;
+        }
+    }
+    // exclusive prefix of the chunk's step maps (Hillis-Steele over the wave)
+    uint32_t inc = map;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t before = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc = map_then<NSM>(before, inc);
+    }
+    uint32_t excl = __shfl_up(inc, 1, kWave);
+    if (lane == 0) excl = kIdentityMap;
+    if (valid) words[row] = (excl & 0x00FFFFFFu) | (traded << 24);
+    if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + blockIdx.x] = inc;
 }
 
-// ------------------------------------------------------------------ path scan
-// Dynamic LDS: [kSeg doubles: selected rewards][nch*ns bytes: end maps][nch bytes: starts]
-template <bool ARL>
-__global__ __launch_bounds__(kScanBlock) void k_path_scan(
+// ------------------------------------------------------------------ table on the matrix cores
+// gfx950's f32-input MFMA v_mfma_f32_16x16x4_f32 computes, per output, the
+// k-ordered fused chain D = fma(a_k3,b_k3, fma(.., fma(a_k0,b_k0, C))) --
+// exactly the canonical dot-product order of the numerics contract -- so the
+// policy's two H-wide layers run on the matrix pipe bit-identically to the
+// VALU/oracle chains, with the weights held as compact per-lane fragments
+// (loaded once per wave, reused for every tile) instead of being streamed
+// through scalar loads.
+//
+// One wave = one 64-tick chunk of one episode, all inventory states:
+// 16-sample tiles (state si, ticks 16q..16q+15 of the chunk).
+//   layer 2:  H2^T[j][n] = W2[j][:] . H1^T[:][n] + b2[j]   (A = W2 rows, B = h1 of
+//             sample n at k = 4i + (lane>>4); C = b2 broadcast)
+//   layer 3:  OUT[o][n] = W3[o][:] . relu(H2^T)[:][n] + b3[o]  (rows o = 0,1 of a
+//             16-row tile; B = the layer-2 accumulator registers as they stand)
+// Rows of W2 are permuted so that row 4g+r of row-tile rt is neuron
+// 16rt + 4r + g: the layer-3 MFMA k-step s = 4rt + r then reads, in lane group
+// g, neuron 4s + g from its own register r of tile rt, i.e. neurons
+// 0,1,2,...,H-1 in order -- the canonical layer-3 chain, with no lane movement.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int H, int NSI, bool ARL>
+__global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
+    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
+    const float* __restrict__ mm, int64_t mm_stride, const float* __restrict__ adv,
+    int64_t adv_stride, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
+    static_assert(H % 16 == 0, "MFMA table needs H multiple of 16");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16;  // 16-neuron row tiles of layer 2
+    constexpr int KS = H / 4;   // k-steps (4 per MFMA)
+    const int e = blockIdx.y;
+    const int32_t T = ep.len[e];
+    const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int32_t t0 = chunk * kChunk;
+    if (t0 >= T) return;  // wave-uniform; no block barriers below
+    const int lane = threadIdx.x & (kWave - 1), grp = lane >> 4, col = lane & 15;
+    const int ns = ARL ? 4 * nsi : nsi;
+    const sgmm_env_params p = params[ep.param[e]];
+    const float* __restrict__ g = mm + (int64_t)ep.genome[e] * mm_stride;
+
+    // ---- per-lane weight fragments (lane-dependent, tile-independent)
+    float w2f[NT][KS];  // A of layer 2: row col of tile rt, k = 4i + grp
+    f32x4 b2c[NT];      // C of layer 2: row 4grp + r of tile rt
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt) {
+        const int jrow = 16 * rt + 4 * (col & 3) + (col >> 2);  // permuted neuron of row col
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + jrow * H + 4 * i + grp];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * r + grp];
+    }
+    float w1f[KS][4];   // layer 1 for k = 4i + grp: W1[k][0..2], b1[k]
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const int k = 4 * i + grp;
+        w1f[i][0] = g[L::W1 + 3 * k];
+        w1f[i][1] = g[L::W1 + 3 * k + 1];
+        w1f[i][2] = g[L::W1 + 3 * k + 2];
+        w1f[i][3] = g[L::B1 + k];
+    }
+    float w3f[KS];      // A of layer 3: row col (= output o), k-step s -> neuron 4s + grp
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2) w3f[s2] = col < 2 ? g[L::W3 + col * H + 4 * s2 + grp] : 0.0f;
+    f32x4 b3c;          // C of layer 3: row 4grp + r = output o
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b3c[r] = (grp == 0 && r < 2) ? g[L::B3 + r] : 0.0f;
+
+    // ---- the policy for every (state, tick) of the chunk.  The NSI states of a
+    // 16-tick group are independent MFMA chains: issuing them interleaved
+    // (k-step outer, state inner) keeps the matrix pipe fed despite the
+    // dependent-accumulator latency of each chain.
+    float out0[NSI], out1[NSI];
+#pragma unroll
+    for (int si = 0; si < NSI; ++si) out0[si] = out1[si] = 0.0f;
+    float x2[NSI];
+#pragma unroll
+    for (int si = 0; si < NSI; ++si) x2[si] = (float)((double)(inv_min + si) / 2.0);
+    float xs0[4], xs1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int tq = min(t0 + 16 * q + col, T - 1);  // clamp: padded samples are discarded
+        const int64_t ti = ep.tick_off[e] + tq;
+        xs0[q] = tk.s1n[ti];
+        xs1[q] = tk.s2n[ti];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        float pre[KS];
+#pragma unroll
+        for (int i = 0; i < KS; ++i)
+            pre[i] = __builtin_fmaf(w1f[i][1], xs1[q], __builtin_fmaf(w1f[i][0], xs0[q], w1f[i][3]));
+        f32x4 acc[NSI][NT];
+#pragma unroll
+        for (int si = 0; si < NSI; ++si)
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) acc[si][rt] = b2c[rt];
+#pragma unroll
+        for (int i = 0; i < KS; ++i) {
+#pragma unroll
+            for (int si = 0; si < NSI; ++si) {
+                const float h1 = relu(__builtin_fmaf(w1f[i][2], x2[si], pre[i]));
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt)
+                    acc[si][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, acc[si][rt], 0, 0, 0);
+            }
+        }
+        f32x4 o[NSI];
+#pragma unroll
+        for (int si = 0; si < NSI; ++si) o[si] = b3c;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+            for (int si = 0; si < NSI; ++si)
+                o[si] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3f[s2], relu(acc[si][s2 >> 2][s2 & 3]),
+                                                             o[si], 0, 0, 0);
+        // rows 0/1 of group 0 hold the outputs of sample col: give tick 16q + c
+        // (lane 16q + c) its pair
+#pragma unroll
+        for (int si = 0; si < NSI; ++si) {
+            const float v0 = __shfl(o[si][0], col, kWave), v1 = __shfl(o[si][1], col, kWave);
+            if (grp == q) {
+                out0[si] = v0;
+                out1[si] = v1;
+            }
+        }
+    }
+
+    // ---- FPT step from every state, one lane per tick
+    const bool valid = t0 + lane < T;
+    const int64_t row = ep.step_off[e] + t0 + lane;
+    __shared__ int32_t lut_s[4][2][32];
+    int32_t* lut0 = lut_s[threadIdx.x >> 6][0];
+    int32_t* lut1 = lut_s[threadIdx.x >> 6][1];
+    if (ARL) {
+        const int ai = ep.adv ? ep.adv[e] : -1;
+        if (lane < ns) {
+            int32_t da = 0, db = 0;
+            if (ai >= 0)
+                adv_delta(adv + (int64_t)ai * adv_stride, p, inv_min + (lane >> 2), (lane >> 1) & 1,
+                          lane & 1, da, db);
+            lut0[lane] = da;
+            lut1[lane] = db;
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
+    uint32_t map = kIdentityMap, traded = 0;
+    uint64_t fw = 0;
+    if (valid) {
+        const int64_t ti = ep.tick_off[e] + t0 + lane;
+        const double mid = tk.mid_next[ti], ask = tk.best_ask[ti], bid = tk.best_bid[ti];
+        const double bmax = tk.buy_max[ti], smin = tk.sell_min[ti];
+        double* __restrict__ R = rew + row * ns;
+        map = 0;
+#pragma unroll
+        for (int si = 0; si < NSI; ++si) {
+            if (si >= nsi) break;
+            const int32_t inv = inv_min + si;
+            const int32_t oa = act_to_int(rintf(out0[si] * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(out1[si] * p.act_scale));
+            if (!ARL) {
+                const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
+                map |= (uint32_t)(si + so.fill_buy - so.fill_sell) << (3 * si);
+                traded |= (uint32_t)(so.fill_buy | so.fill_sell) << si;
+                R[si] = so.reward;
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int s = 4 * si + c;
+                    const StepOut so = ftp_step(p, inv, oa + lut0[s], ob + lut1[s], mid, ask, bid,
+                                                bmax, smin);
+                    fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * s);
+                    R[s] = so.reward;
+                }
+            }
+        }
+    }
+    if (ARL) {
+        if (valid) fills[row] = fw;
+        return;
+    }
+    uint32_t inc = map;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t before = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc = map_then<(NSI < 8 ? NSI : 8)>(before, inc);
+    }
+    uint32_t excl = __shfl_up(inc, 1, kWave);
+    if (lane == 0) excl = kIdentityMap;
+    if (valid) words[row] = (excl & 0x00FFFFFFu) | (traded << 24);
+    if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + chunk] = inc;
+}
+
+// ------------------------------------------------------------------ path scan (no adversary)
+// One workgroup (16 waves) per episode.
+//   1. all waves: the episode's prefix words -> LDS (one coalesced pass);
+//      wave 0: chunk start states from a wave-level scan of the chunk maps;
+//   2. waves 1..15 (producers): per tick, state = one field of its prefix word,
+//      gather the reward of that state into LDS sel[t], count trades, and
+//      publish each finished 256-tick segment with an LDS counter;
+//   3. thread 0 (consumer): adds sel[] in tick order as segments become
+//      ready (drl_engine.py:54: total = ((r0 + r1) + r2) + ..., float64) --
+//      the only serial part of the rollout, fed from LDS three loads ahead.
+// Episodes longer than kScanWin ticks are processed in windows with a
+// workgroup barrier between windows.
+constexpr int kScanThreads = 1024;
+
+#ifdef SGMM_STAMPS
+// diagnostic build only: per-episode phase timestamps of the scan kernel
+__device__ unsigned long long g_stamps[4096][8];
+#define SGMM_STAMP(e, k)                                                           \
+    do {                                                                           \
+        unsigned long long t_;                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        if (threadIdx.x == 0 && (e) < 4096) g_stamps[e][k] = t_;                   \
+    } while (0)
+#else
+#define SGMM_STAMP(e, k) \
+    do {                 \
+    } while (0)
+#endif
+constexpr int kScanWin = 4096;         // ticks resident per window (32 KB of rewards)
+constexpr int kReadySeg = 256;         // ticks per ready counter
+
+template <int NSM>
+__global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
+    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
+    const uint32_t* __restrict__ words, const uint32_t* __restrict__ cmaps,
+    const double* __restrict__ rew, double* __restrict__ fitness,
+    int32_t* __restrict__ trades_out) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    double* sel = reinterpret_cast<double*>(lds);                          // [kScanWin]
+    uint32_t* wl = reinterpret_cast<uint32_t*>(sel + kScanWin);            // [kScanWin]
+    uint8_t* start = reinterpret_cast<uint8_t*>(wl + kScanWin);            // [nch]
+    __shared__ int ready[kScanWin / kReadySeg];
+    __shared__ int red_trades;
+    const int e = blockIdx.x;
+    const int32_t T = ep.len[e];
+    const int nch = (T + kChunk - 1) / kChunk;
+    const int64_t so = ep.step_off[e];
+    const uint32_t cb = chunk_base(so, e);
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
+    if (tid == 0) red_trades = 0;
+    SGMM_STAMP(e, 0);
+    if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
+        uint32_t s = (uint32_t)(-inv_min);
+        for (int c0 = 0; c0 < nch; c0 += kWave) {
+            const int c = c0 + lane;
+            const uint32_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
+            uint32_t inc = m;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t before = __shfl_up(inc, d, kWave);
+                if (lane >= d) inc = map_then<NSM>(before, inc);
+            }
+            uint32_t excl = __shfl_up(inc, 1, kWave);
+            if (lane == 0) excl = kIdentityMap;
+            if (c < nch) start[c] = (uint8_t)map_get(excl, s);
+            s = map_get(__shfl(inc, kWave - 1, kWave), s);
+        }
+    }
+    SGMM_STAMP(e, 1);
+    const int ns = nsi;
+    int my_trades = 0;
+    double total = 0.0;
+    for (int w0 = 0; w0 < T; w0 += kScanWin) {
+        const int n = min(kScanWin, T - w0);
+        // prefix words of the window -> LDS; clear the ready counters
+        for (int i = tid; i < n; i += kScanThreads) wl[i] = words[so + w0 + i];
+        if (tid < kScanWin / kReadySeg) ready[tid] = 0;
+        __syncthreads();
+        SGMM_STAMP(e, 2);
+        if (tid >= kWave) {
+            // producers: wave w covers 64 consecutive ticks per pass (one ready
+            // segment), all of a thread's reward gathers issued before any write
+            constexpr int kPass = kScanThreads - kWave;  // 960 ticks per pass
+            constexpr int kMaxPass = (kScanWin + kPass - 1) / kPass;
+            const int i0 = tid - kWave;
+            double r[kMaxPass];
+            uint32_t stv[kMaxPass], wdv[kMaxPass];
+#pragma unroll
+            for (int k = 0; k < kMaxPass; ++k) {
+                const int i = i0 + k * kPass;
+                if (i < n) {
+                    const int t = w0 + i;
+                    wdv[k] = wl[i];
+                    stv[k] = map_get(wdv[k], start[t / kChunk]);
+                    r[k] = rew[(so + t) * ns + stv[k]];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kMaxPass; ++k) {
+                const int i = i0 + k * kPass;
+                if (k * kPass + (i0 & ~(kWave - 1)) >= n) break;  // whole wave past the end
+                const bool ok = i < n;
+                if (ok) {
+                    sel[i] = r[k];
+                    my_trades += (wdv[k] >> (24 + stv[k])) & 1u;
+                }
+                const int cnt = __popcll(__ballot(ok));
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                if (lane == 0)
+                    __hip_atomic_fetch_add(&ready[(i & ~(kWave - 1)) / kReadySeg], cnt,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else if (tid == 0) {
+            for (int sg = 0; sg * kReadySeg < n; ++sg) {
+                const int b = sg * kReadySeg, m = min(kReadySeg, n - b);
+                while (__hip_atomic_load(&ready[sg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < m)
+                    __builtin_amdgcn_s_sleep(1);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                const double* buf = sel + b;
+                int t = 0;
+                if (m == kReadySeg) {
+                    // two 8-value register groups: LDS reads run 16 values ahead of the adds
+                    double2 a0 = *reinterpret_cast<const double2*>(buf + 0);
+                    double2 a1 = *reinterpret_cast<const double2*>(buf + 2);
+                    double2 a2 = *reinterpret_cast<const double2*>(buf + 4);
+                    double2 a3 = *reinterpret_cast<const double2*>(buf + 6);
+                    double2 b0 = *reinterpret_cast<const double2*>(buf + 8);
+                    double2 b1 = *reinterpret_cast<const double2*>(buf + 10);
+                    double2 b2 = *reinterpret_cast<const double2*>(buf + 12);
+                    double2 b3 = *reinterpret_cast<const double2*>(buf + 14);
+#pragma unroll 1
+                    for (t = 16; t < kReadySeg; t += 16) {
+                        total += a0.x; total += a0.y; total += a1.x; total += a1.y;
+                        total += a2.x; total += a2.y; total += a3.x; total += a3.y;
+                        a0 = *reinterpret_cast<const double2*>(buf + t);
+                        a1 = *reinterpret_cast<const double2*>(buf + t + 2);
+                        a2 = *reinterpret_cast<const double2*>(buf + t + 4);
+                        a3 = *reinterpret_cast<const double2*>(buf + t + 6);
+                        total += b0.x; total += b0.y; total += b1.x; total += b1.y;
+                        total += b2.x; total += b2.y; total += b3.x; total += b3.y;
+                        b0 = *reinterpret_cast<const double2*>(buf + t + 8);
+                        b1 = *reinterpret_cast<const double2*>(buf + t + 10);
+                        b2 = *reinterpret_cast<const double2*>(buf + t + 12);
+                        b3 = *reinterpret_cast<const double2*>(buf + t + 14);
+                    }
+                    total += a0.x; total += a0.y; total += a1.x; total += a1.y;
+                    total += a2.x; total += a2.y; total += a3.x; total += a3.y;
+                    total += b0.x; total += b0.y; total += b1.x; total += b1.y;
+                    total += b2.x; total += b2.y; total += b3.x; total += b3.y;
+                } else {
+                    for (; t < m; ++t) total += buf[t];
+                }
+                if (sg == 0) SGMM_STAMP(e, 3);
+            }
+            SGMM_STAMP(e, 4);
+        }
+        __syncthreads();
+    }
+    SGMM_STAMP(e, 5);
+    int wsum = my_trades;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+    if (lane == 0 && wsum) atomicAdd(&red_trades, wsum);
+    __syncthreads();
+    if (tid == 0) {
+        const int tr = red_trades;
+        if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
+        fitness[e] = total;
+        trades_out[e] = tr;
+    }
+}
+
+// ------------------------------------------------------------------ path scan (adversary)
+// 20-state transducer (inventory x previous fills): every chunk is walked from
+// every start state, the chunk end-maps are chained, each chunk is replayed
+// from its true start.  Dynamic LDS: [kSeg doubles][nch*ns end maps][nch starts]
+__device__ __forceinline__ int next_state_arl(int s, int code) {
+    const int fb = code & 1, fs = code >> 1;
+    return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
     const uint64_t* __restrict__ fills, const double* __restrict__ rew,
     double* __restrict__ fitness, int32_t* __restrict__ trades_out) {
@@ -149,7 +576,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan(
     double* sel = reinterpret_cast<double*>(lds);
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
-    const int ns = ARL ? 4 * nsi : nsi;
+    const int ns = 4 * nsi;
     const int nch = (T + kChunk - 1) / kChunk;
     uint8_t* endmap = lds + kSeg * sizeof(double);
     uint8_t* start = endmap + nch * ns;
@@ -159,27 +586,22 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan(
     const double* __restrict__ R = rew + so * ns;
     const int tid = threadIdx.x;
     if (tid == 0) red_trades = 0;
-
-    // phase 1: end state of every chunk from every start state
     for (int i = tid; i < nch * ns; i += kScanBlock) {
         const int k = i / ns;
         int s = i - k * ns;
         const int ta = k * kChunk, tb = min(T, ta + kChunk);
-        for (int t = ta; t < tb; ++t) s = next_state(s, (int)(F[t] >> (2 * s)) & 3, ARL);
+        for (int t = ta; t < tb; ++t) s = next_state_arl(s, (int)(F[t] >> (2 * s)) & 3);
         endmap[i] = (uint8_t)s;
     }
     __syncthreads();
-    // phase 2: chain the chunk maps from the initial state (inventory 0, no fills)
     if (tid == 0) {
-        int s = ARL ? (-inv_min) << 2 : -inv_min;
+        int s = (-inv_min) << 2;
         for (int k = 0; k < nch; ++k) {
             start[k] = (uint8_t)s;
             s = endmap[k * ns + s];
         }
     }
     __syncthreads();
-    // phases 3+4 per segment: replay chunks from their true start selecting the
-    // reward of the visited state, then sum in tick order.
     double total = 0.0;
     int my_trades = 0;
     for (int seg0 = 0; seg0 < T; seg0 += kSeg) {
@@ -193,26 +615,14 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan(
                 const int code = (int)(F[t] >> (2 * s)) & 3;
                 sel[t - seg0] = R[(int64_t)t * ns + s];
                 my_trades += (code != 0);
-                s = next_state(s, code, ARL);
+                s = next_state_arl(s, code);
             }
         }
         __syncthreads();
-        if (tid == 0) {
-            // reference order: total = ((r0 + r1) + r2) + ... (drl_engine.py:54)
-            int t = 0;
-            for (; t + 8 <= segn; t += 8) {
-                const double2 a = *reinterpret_cast<const double2*>(sel + t);
-                const double2 b = *reinterpret_cast<const double2*>(sel + t + 2);
-                const double2 c = *reinterpret_cast<const double2*>(sel + t + 4);
-                const double2 d = *reinterpret_cast<const double2*>(sel + t + 6);
-                total += a.x; total += a.y; total += b.x; total += b.y;
-                total += c.x; total += c.y; total += d.x; total += d.y;
-            }
-            for (; t < segn; ++t) total += sel[t];
-        }
+        if (tid == 0)
+            for (int t = 0; t < segn; ++t) total += sel[t];
         __syncthreads();
     }
-    // trades: integer, any order
     int w = my_trades;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) w += __shfl_xor(w, off, kWave);
@@ -220,7 +630,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan(
     __syncthreads();
     if (tid == 0) {
         const int tr = red_trades;
-        if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
+        if (tr == 0) total -= params[ep.param[e]].idle_penalty;
         fitness[e] = total;
         trades_out[e] = tr;
     }
@@ -424,29 +834,77 @@ static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Table kernel selection: 0 = f32 MFMA (default for H >= 16), 1 = VALU
+// (one lane per (tick, state)).  SGMM_TABLE_PATH=valu forces the VALU kernel
+// (A/B measurements and as an independent cross-check in the tests).
+static int table_path() {
+    const char* e = std::getenv("SGMM_TABLE_PATH");
+    return (e && std::strcmp(e, "valu") == 0) ? 1 : 0;
+}
+
 }  // namespace sgmm
 
 using namespace sgmm;
 
+#ifdef SGMM_STAMPS
+extern "C" int sgmm_debug_stamps(unsigned long long* host, int n_eps) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n_eps);
+}
+#endif
+
+// Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
+//   u32 words[total_steps] | u32 cmaps[total_steps/64 + n + 1] (no adversary)
+//   u64 fills[total_steps]                                  (adversary)
+//   f64 rew[total_steps * n_states]
+static size_t ws_words(int64_t steps) { return align256((size_t)steps * sizeof(uint32_t)); }
+static size_t ws_cmaps(int32_t n, int64_t steps) {
+    return align256(((size_t)steps / kChunk + (size_t)n + 1) * sizeof(uint32_t));
+}
+static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
+
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
                                               int32_t n_states) {
-    (void)n_episodes;
-    if (total_steps < 0 || n_states <= 0) return 0;
-    return align256((size_t)total_steps * sizeof(uint64_t)) +
-           align256((size_t)total_steps * (size_t)n_states * sizeof(double));
+    if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
+    const size_t head = n_states > 8 ? ws_fills(total_steps)
+                                     : ws_words(total_steps) + ws_cmaps(n_episodes, total_steps);
+    return head + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
 }
 
 template <int H>
-static void launch_table(bool arl, dim3 grid, hipStream_t s, const sgmm_ticks& tk,
+static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
+                              const sgmm_ticks& tk, const EpArrays& ep,
+                              const sgmm_env_params* params, const float* mm, int64_t mm_stride,
+                              const float* adv, int64_t adv_stride, int32_t inv_min,
+                              uint32_t* words, uint32_t* cmaps, uint64_t* fills, double* rew) {
+    const int nch = (max_len + kChunk - 1) / kChunk;
+    const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
+#define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
+    hipLaunchKernelGGL((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
+                       mm, mm_stride, adv, adv_stride, inv_min, nsi, words, cmaps, fills, rew)
+    if (arl) {
+        if (nsi <= 5) SGMM_TABLE_MFMA(5, true);
+        else SGMM_TABLE_MFMA(8, true);
+    } else if (nsi <= 5) {
+        SGMM_TABLE_MFMA(5, false);
+    } else {
+        SGMM_TABLE_MFMA(8, false);
+    }
+#undef SGMM_TABLE_MFMA
+}
+
+template <int H>
+static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm_ticks& tk,
                          const EpArrays& ep, const sgmm_env_params* params, const float* mm,
                          int64_t mm_stride, const float* adv, int64_t adv_stride, int32_t inv_min,
-                         int32_t nsi, uint64_t* fills, double* rew) {
-    if (arl)
-        hipLaunchKernelGGL((k_policy_table<H, true>), grid, dim3(kTableBlock), 0, s, tk, ep,
-                           params, mm, mm_stride, adv, adv_stride, inv_min, nsi, fills, rew);
-    else
-        hipLaunchKernelGGL((k_policy_table<H, false>), grid, dim3(kTableBlock), 0, s, tk, ep,
-                           params, mm, mm_stride, adv, adv_stride, inv_min, nsi, fills, rew);
+                         uint32_t* words, uint32_t* cmaps, uint64_t* fills, double* rew) {
+    const dim3 block(kChunk * nsi);  // one wave per inventory state
+#define SGMM_TABLE(NSM_, ARL_)                                                                  \
+    hipLaunchKernelGGL((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, mm,  \
+                       mm_stride, adv, adv_stride, inv_min, nsi, words, cmaps, fills, rew)
+    if (arl) SGMM_TABLE(8, true);
+    else if (nsi <= 5) SGMM_TABLE(5, false);
+    else SGMM_TABLE(8, false);
+#undef SGMM_TABLE
 }
 
 extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes* eps,
@@ -468,29 +926,58 @@ extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes
         set_error("workspace %zu bytes < required %zu", workspace_bytes, need);
         return SGMM_ERR_WORKSPACE;
     }
-    uint64_t* fills = reinterpret_cast<uint64_t*>(workspace);
-    double* rew = reinterpret_cast<double*>(reinterpret_cast<char*>(workspace) +
-                                            align256((size_t)eps->total_steps * sizeof(uint64_t)));
+    char* w = reinterpret_cast<char*>(workspace);
+    uint32_t* words = nullptr;
+    uint32_t* cmaps = nullptr;
+    uint64_t* fills = nullptr;
+    double* rew;
+    if (arl) {
+        fills = reinterpret_cast<uint64_t*>(w);
+        rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
+    } else {
+        words = reinterpret_cast<uint32_t*>(w);
+        cmaps = reinterpret_cast<uint32_t*>(w + ws_words(eps->total_steps));
+        rew = reinterpret_cast<double*>(w + ws_words(eps->total_steps) +
+                                        ws_cmaps(eps->n, eps->total_steps));
+    }
     hipStream_t s = as_stream(stream);
     const EpArrays ep = ep_arrays(eps, arl);
     if (eps->max_len > 0) {
-        dim3 grid((eps->max_len + kTableBlock - 1) / kTableBlock, eps->n);
+        dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
+        ProfScope prof("policy_table", s);
+        const bool valu = table_path() == 1;
         switch (hidden) {
-            case 8: launch_table<8>(arl, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, fills, rew); break;
-            case 16: launch_table<16>(arl, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, fills, rew); break;
-            case 32: launch_table<32>(arl, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, fills, rew); break;
-            default: launch_table<64>(arl, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, fills, rew); break;
+            case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew); break;
+            case 16:
+                if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                break;
+            case 32:
+                if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                break;
+            default:
+                if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<64>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                break;
         }
         SGMM_LAUNCHED();
     }
     const int nch_max = (eps->max_len + kChunk - 1) / kChunk;
-    const size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
-    if (arl)
-        hipLaunchKernelGGL(k_path_scan<true>, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
+    ProfScope prof("path_scan", s);
+    if (arl) {
+        const size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
+        hipLaunchKernelGGL(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades);
-    else
-        hipLaunchKernelGGL(k_path_scan<false>, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
-                           eps->inv_min, nsi, fills, rew, fitness, trades);
+    } else {
+        const size_t lds = kScanWin * (sizeof(double) + sizeof(uint32_t)) + nch_max;
+        if (nsi <= 5)
+            hipLaunchKernelGGL(k_path_scan_maps<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
+                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades);
+        else
+            hipLaunchKernelGGL(k_path_scan_maps<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
+                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades);
+    }
     SGMM_LAUNCHED();
     return SGMM_OK;
 }
@@ -515,6 +1002,7 @@ extern "C" int sgmm_rollout_trace(const sgmm_ticks* ticks, const sgmm_episodes* 
                fill_buy, fill_sell, raw_a, raw_b, fitness, trades};
     const EpArrays ep = ep_arrays(eps, arl);
     hipStream_t s = as_stream(stream);
+    ProfScope prof("rollout_direct", s);
     switch (hidden) {
         case 8: hipLaunchKernelGGL(k_rollout_direct<8>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
         case 16: hipLaunchKernelGGL(k_rollout_direct<16>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
@@ -536,6 +1024,7 @@ extern "C" int sgmm_policy_forward(const float* genomes, int64_t genome_stride, 
     if (n == 0) return SGMM_OK;
     const dim3 grid((unsigned)((n + 255) / 256)), blk(256);
     hipStream_t s = as_stream(stream);
+    ProfScope prof("policy_forward", s);
     switch (hidden) {
         case 8: hipLaunchKernelGGL(k_policy_forward<8>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
         case 16: hipLaunchKernelGGL(k_policy_forward<16>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
@@ -553,6 +1042,7 @@ extern "C" int sgmm_adversary_forward(const float* genomes, int64_t genome_strid
     SGMM_REQUIRE(genomes && states && out, "null pointer");
     SGMM_REQUIRE(n >= 0 && genome_stride >= 74, "bad n or stride");
     if (n == 0) return SGMM_OK;
+    ProfScope prof("adversary_forward", as_stream(stream));
     hipLaunchKernelGGL(k_adversary_forward, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        as_stream(stream), genomes, genome_stride, genome_idx, states, out, n);
     SGMM_LAUNCHED();
@@ -573,6 +1063,7 @@ extern "C" int sgmm_env_step_batch(const sgmm_env_params* params, const int32_t*
                  "null pointer");
     SGMM_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return SGMM_OK;
+    ProfScope prof("env_step", as_stream(stream));
     hipLaunchKernelGGL(k_env_step, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        as_stream(stream), params, param_idx, inventory, cash, action, adv_action,
                        mid_next, best_ask, best_bid, buy_max, sell_min, reward, pnl_reward,

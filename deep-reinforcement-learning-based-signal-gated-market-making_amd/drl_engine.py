@@ -154,12 +154,14 @@ class DRLEngine:
       dist        -- torch.distributed group (None = default if initialised,
                      False = single process): the population is sharded over ranks
                      and fitness is all-gathered once per generation.
+      use_graph   -- capture one generation in a HIP graph and replay it
+                     (single process, rng="device").
     """
 
     def __init__(self, pop_size=50, sigma=0.05, phi=0.01, tick_size=0.01, fee_rate=0.0,
                  use_arl=False, save_dir="checkpoints/drl", *, hidden_dim=32, rng="device",
                  seed=None, val_mode="auto", honor_sigma=False, sync_every=10, dist=None,
-                 device=None, verbose=True, patience=15, decay=0.5):
+                 device=None, verbose=True, patience=15, decay=0.5, use_graph=True):
         self.phi = phi
         self.tick_size = tick_size
         self.fee_rate = fee_rate
@@ -178,8 +180,10 @@ class DRLEngine:
         if rng not in ("device", "torch"):
             raise ValueError("rng must be 'device' or 'torch'")
         self.rng = rng
-        self.seed = int(seed) if seed is not None else int(torch.randint(0, 2**62, (1,)).item()) \
-            if rng == "device" else 0
+        if seed is not None:
+            self.seed = int(seed)
+        else:  # rng="torch" must not draw extra numbers from the reference stream
+            self.seed = int(torch.randint(0, 2**62, (1,)).item()) if rng == "device" else 0
         self.val_mode = val_mode
         self.sync_every = max(1, int(sync_every))
         self.dist = dist
@@ -187,166 +191,248 @@ class DRLEngine:
         self.verbose = verbose
         self.patience = int(patience)
         self.decay = float(decay)
+        self.use_graph = use_graph
         self.timing = {}
 
-    # ------------------------------------------------------------------ helpers
     def _log(self, msg):
         if self.verbose:
             print(msg)
             sys.stdout.flush()
 
+    def session(self, train_bundle, val_bundle, train_stats, generations=100, output_prefix="agent"):
+        """Device-resident training session: step(gen) enqueues one generation."""
+        return TrainingSession(self, train_bundle, val_bundle, train_stats, generations, output_prefix)
+
     def train(self, train_bundle, val_bundle, train_stats, generations=100, output_prefix="agent"):
+        sess = self.session(train_bundle, val_bundle, train_stats, generations, output_prefix)
+        for gen in range(generations):
+            sess.step(gen)
+            if (gen + 1) % self.sync_every == 0:
+                sess.flush(gen + 1)
+        return sess.finish()
+
+
+class TrainingSession:
+    """One DRLEngine.train run, resident on the GPU (drl_engine.py:83-178).
+
+    Per generation (step): ask the shard's genomes -> roll the shard out (train,
+    plus validation when fused) -> all-gather fitness over ranks -> tell both
+    evolvers -> validation bookkeeping (checkpoint slot, sigma decay, history).
+    Nothing in step() waits for the device; flush() brings history rows to the
+    host, prints the reference's log lines in order and writes the checkpoint."""
+
+    def __init__(self, eng: DRLEngine, train_bundle, val_bundle, train_stats, generations, output_prefix):
         _lib.require_gpu()
-        eng = _engine(self.device)
-        dev = eng.device
-        L = eng.L
-        group, rank, world = _dist_info(self.dist)
-        P, H = self.pop_size, self.hidden_dim
-        G = genome_size(H)
-        i0, i1 = shard_bounds(P, rank, world)
-        n_loc = i1 - i0
-        arl = self.use_arl
-        fused = self.val_mode == "fused" or (self.val_mode == "auto" and n_loc <= 512)
-        torch_rng = self.rng == "torch"
+        self.e = eng
+        # a session owns its workspace: a captured graph keeps raw pointers to it
+        self.roll = RolloutEngine(eng.device or "cuda")
+        dev = self.dev = self.roll.device
+        self.L = self.roll.L
+        self.group, self.rank, self.world = _dist_info(eng.dist)
+        P, H = eng.pop_size, eng.hidden_dim
+        self.P, self.H, self.G = P, H, genome_size(H)
+        G = self.G
+        self.i0, self.i1 = shard_bounds(P, self.rank, self.world)
+        n_loc = self.n_loc = self.i1 - self.i0
+        arl = self.arl = eng.use_arl
+        self.fused = eng.val_mode == "fused" or (eng.val_mode == "auto" and n_loc <= 512)
+        self.torch_rng = eng.rng == "torch"
+        self.generations = int(generations)
         # (rng="torch" with world > 1: every rank draws the identical full
         # population from its identically seeded generator)
-
-        ticks = device_ticks([train_bundle, val_bundle], train_stats, dev)
-        (tr_off, T_tr), (va_off, T_va) = ticks.segments
-        params = params_tensor([EnvConfig(phi=self.phi, tick_size=self.tick_size,
-                                          fee_rate=self.fee_rate)], dev)
-        # episode batches: training shard (+ fused validation of the shard)
-        if fused and not arl:
-            train_eps = EpisodeBatch(np.concatenate([np.arange(n_loc), np.arange(n_loc)]),
-                                     np.concatenate([np.full(n_loc, tr_off), np.full(n_loc, va_off)]),
-                                     np.concatenate([np.full(n_loc, T_tr), np.full(n_loc, T_va)]),
-                                     np.zeros(2 * n_loc)).to(dev)
-            val_eps = None
+        self.ticks = device_ticks([train_bundle, val_bundle], train_stats, dev)
+        (tr_off, self.T_tr), (va_off, self.T_va) = self.ticks.segments
+        self.params = params_tensor([EnvConfig(phi=eng.phi, tick_size=eng.tick_size,
+                                               fee_rate=eng.fee_rate)], dev)
+        if self.fused and not arl:  # one launch: training + validation episodes of the shard
+            self.train_eps = EpisodeBatch(
+                np.concatenate([np.arange(n_loc), np.arange(n_loc)]),
+                np.concatenate([np.full(n_loc, tr_off), np.full(n_loc, va_off)]),
+                np.concatenate([np.full(n_loc, self.T_tr), np.full(n_loc, self.T_va)]),
+                np.zeros(2 * n_loc)).to(dev)
+            self.val_eps = None
         else:
-            train_eps = EpisodeBatch(np.arange(n_loc), np.full(n_loc, tr_off), np.full(n_loc, T_tr),
-                                     np.zeros(n_loc), adv=np.arange(n_loc) if arl else None).to(dev)
-            nv = n_loc if fused else 1
-            val_eps = EpisodeBatch(np.arange(nv), np.full(nv, va_off), np.full(nv, T_va), np.zeros(nv)).to(dev)
-
+            self.train_eps = EpisodeBatch(np.arange(n_loc), np.full(n_loc, tr_off), np.full(n_loc, self.T_tr),
+                                          np.zeros(n_loc), adv=np.arange(n_loc) if arl else None).to(dev)
+            nv = n_loc if self.fused else 1
+            self.val_eps = EpisodeBatch(np.arange(nv), np.full(nv, va_off), np.full(nv, self.T_va),
+                                        np.zeros(nv)).to(dev)
         f32 = dict(dtype=torch.float32, device=dev)
-        pop = torch.empty((P if torch_rng else n_loc, G), **f32)
-        pop_loc = pop[i0:i1] if torch_rng else pop
-        adv_pop = torch.empty((P if torch_rng else n_loc, ADV_GENOME), **f32) if arl else None
-        adv_loc = (adv_pop[i0:i1] if torch_rng else adv_pop) if arl else None
-        master = self.mm_evolver.master_policy.get_weights().to(**f32)
-        master_adv = self.adv_evolver.master_policy.get_weights().to(**f32) if arl else None
-        best_master = torch.zeros(G, **f32)
-        state = torch.zeros(ctypes_size(GAState), dtype=torch.uint8, device=dev)
-        hist = torch.zeros((generations, ctypes_size(GAHistory)), dtype=torch.uint8, device=dev)
-        n_out = train_eps.n
-        out = (torch.empty(n_out, dtype=torch.float64, device=dev),
-               torch.empty(n_out, dtype=torch.int32, device=dev))
-        vout = (torch.empty(val_eps.n, dtype=torch.float64, device=dev),
-                torch.empty(val_eps.n, dtype=torch.int32, device=dev)) if val_eps is not None else None
-        # full-population views (gathered when world > 1)
-        n_max = shard_bounds(P, 0, world)[1]
-        gbuf = torch.empty((world, 4, n_max), dtype=torch.float64, device=dev) if world > 1 else None
-        s = stream_ptr()
-        check(L.sgmm_ga_state_init(ptr(state), float(self.mm_evolver.sigma), self.patience, self.decay, s),
-              "sgmm_ga_state_init")
-        if arl and self.adv_evolver.sigma != self.mm_evolver.sigma:
+        n_pop = P if self.torch_rng else n_loc
+        self.pop = torch.empty((n_pop, G), **f32)
+        self.pop_loc = self.pop[self.i0:self.i1] if self.torch_rng else self.pop
+        self.adv_pop = torch.empty((n_pop, ADV_GENOME), **f32) if arl else None
+        self.adv_loc = (self.adv_pop[self.i0:self.i1] if self.torch_rng else self.adv_pop) if arl else None
+        self.master = eng.mm_evolver.master_policy.get_weights().to(**f32)
+        self.master_adv = eng.adv_evolver.master_policy.get_weights().to(**f32) if arl else None
+        self.best_master = torch.zeros(G, **f32)
+        self.state = torch.zeros(HIST_STATE_SIZES[0], dtype=torch.uint8, device=dev)
+        self.hist = torch.zeros((self.generations, HIST_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.out = (torch.empty(self.train_eps.n, dtype=torch.float64, device=dev),
+                    torch.empty(self.train_eps.n, dtype=torch.int32, device=dev))
+        self.vout = (torch.empty(self.val_eps.n, dtype=torch.float64, device=dev),
+                     torch.empty(self.val_eps.n, dtype=torch.int32, device=dev)) if self.val_eps else None
+        n_max = shard_bounds(P, 0, self.world)[1]
+        self.gbuf = torch.empty((self.world, 4, n_max), dtype=torch.float64, device=dev) \
+            if self.world > 1 else None
+        if arl and eng.adv_evolver.sigma != eng.mm_evolver.sigma:
             raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
-        sig_mm = ptr(state)  # sigma_mm is the first field of sgmm_ga_state
-        sig_adv = ctypes_offset_ptr(state, GAState.sigma_adv.offset)
-        best_path = os.path.join(self.save_dir, f"{output_prefix}_best_val_{self.phi}.pth")
-        saved_any = False
-        emitted = 0
-        history = {"gen": [], "train_f": [], "val_f": [], "train_trades": [], "val_trades": []}
-        ev_start, ev_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev_start.record()
+        check(self.L.sgmm_ga_state_init(ptr(self.state), float(eng.mm_evolver.sigma), eng.patience,
+                                        eng.decay, stream_ptr()), "sgmm_ga_state_init")
+        # generation boundary in one launch (tell + validation + next ask) when the
+        # population is drawn on device and validated in the training launch
+        self.fast_step = (not self.torch_rng and self.fused and G <= 4096 and ADV_GENOME <= 4096
+                          and n_loc * G <= (1 << 22))
+        if self.fast_step:  # the ask of generation 0; later asks happen inside ga_step
+            check(self.L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, eng.seed, self.i0, n_loc,
+                                     ptr(self.pop), G, stream_ptr()), "sgmm_ga_ask")
+            if arl:
+                check(self.L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, eng.seed,
+                                         self.i0, n_loc, ptr(self.adv_pop), ADV_GENOME, stream_ptr()),
+                      "sgmm_ga_ask(adv)")
+        # one generation = fixed launches -> replayable graph (eager when the host
+        # draws the population or a collective sits inside the generation)
+        self.use_graph = bool(eng.use_graph) and not self.torch_rng and self.world == 1
+        self.graph = None
+        self.roll.reserve(self.train_eps, arl)
+        if self.val_eps is not None:
+            self.roll.reserve(self.val_eps, False)
+        self.best_path = os.path.join(eng.save_dir, f"{output_prefix}_best_val_{eng.phi}.pth")
+        self.saved_any = False
+        self.emitted = 0
+        self.history = {"gen": [], "train_f": [], "val_f": [], "train_trades": [], "val_trades": []}
+        self.ev0 = torch.cuda.Event(enable_timing=True)
+        self.ev1 = torch.cuda.Event(enable_timing=True)
+        self.ev0.record()
 
-        def flush(upto):
-            nonlocal emitted, saved_any
-            if upto <= emitted:
-                return
-            rows = hist[emitted:upto].cpu().numpy().view(HIST_DTYPE).reshape(-1)
-            improved_any = False
-            for k, r in enumerate(rows):
-                g = emitted + k
-                imp = bool(r["flags"] & 1)
-                improved_any |= imp
-                if r["flags"] & 2:
-                    self._log(f">>> Sigma decayed to {r['sigma_after']:.4f} due to no improvement")
-                history["gen"].append(g)
-                history["train_f"].append(np.float64(r["train_f"]))
-                history["val_f"].append(np.float64(r["val_f"]))
-                history["train_trades"].append(int(r["train_trades"]))
-                history["val_trades"].append(int(r["val_trades"]))
-                if g % 5 == 0:
-                    tag = "ARL:ON" if arl else "ARL:OFF"
-                    self._log(f"Gen {g:03d} | {tag} | Best Train: {r['train_f']:.2f} | "
-                              f"Val: {r['val_f']:.2f}{'*' if imp else ''}")
-            if improved_any and rank == 0:
-                torch.save(genome_to_state_dict(best_master, H), best_path)
-            saved_any |= improved_any
-            emitted = upto
+    def step(self, gen: int):
+        """Enqueue generation ``gen`` (drl_engine.py:92-171) on the current stream.
 
-        for gen in range(generations):
-            # 1. ask (models/model.py:65-71)
-            if torch_rng:
-                st_now = state.cpu().numpy().view(STATE_DTYPE)[0]
-                pop.copy_(_host_ask(master, float(st_now["sigma_mm"]), P))
-                if arl:
-                    adv_pop.copy_(_host_ask(master_adv, float(st_now["sigma_adv"]), P))
-            else:
-                check(L.sgmm_ga_ask(ptr(master), G, sig_mm, self.seed, 0, gen, i0, n_loc, ptr(pop), G, s),
-                      "sgmm_ga_ask")
-                if arl:
-                    check(L.sgmm_ga_ask(ptr(master_adv), ADV_GENOME, sig_adv, self.seed, 1, gen, i0, n_loc,
-                                        ptr(adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
-            # 2. rollout of the shard (drl_engine.py:104-115)
-            eng.fitness(ticks, train_eps, params, pop_loc, H, adv_loc, out=out)
-            if fused and val_eps is not None:
-                eng.fitness(ticks, val_eps, params, pop_loc, H, None, out=vout)
-            if fused and not arl:
-                tr_f, tr_t, va_f, va_t = out[0][:n_loc], out[1][:n_loc], out[0][n_loc:], out[1][n_loc:]
-            elif fused:
-                tr_f, tr_t, va_f, va_t = out[0], out[1], vout[0], vout[1]
-            else:
-                tr_f, tr_t, va_f, va_t = out[0], out[1], None, None
-            # 3. all-gather the shards' fitness (one collective per generation)
-            if world > 1:
-                tr_f, tr_t, va_f, va_t = _gather(gbuf, tr_f, tr_t, va_f, va_t, P, world, group)
-            # 4. tell both evolvers (model.py:73-76, drl_engine.py:119-125)
-            check(L.sgmm_ga_tell(ptr(state), ptr(tr_f), ptr(tr_t), P, ptr(master),
-                                 ptr(pop) if torch_rng else None, G,
-                                 ptr(master_adv) if arl else None,
-                                 ptr(adv_pop) if (arl and torch_rng) else None, ADV_GENOME, G,
-                                 ADV_GENOME if arl else 0, self.seed, gen,
-                                 ctypes_offset_ptr(hist, gen * HIST_DTYPE.itemsize), s), "sgmm_ga_tell")
-            # 5. validation of the best (drl_engine.py:129-140)
-            if not fused:
-                eng.fitness(ticks, val_eps, params, master.view(1, G), H, None, out=vout)
-                va_f, va_t = vout
-            check(L.sgmm_ga_val_update(ptr(state), ptr(va_f), ptr(va_t), 1 if fused else 0, ptr(master),
-                                       ptr(best_master), G, ctypes_offset_ptr(hist, gen * HIST_DTYPE.itemsize),
-                                       s), "sgmm_ga_val_update")
-            if torch_rng:
-                TradingPolicy()  # the reference's validation builds a TradingPolicy() (RNG draw)
-            if (gen + 1) % self.sync_every == 0:
-                flush(gen + 1)
-        ev_end.record()
-        flush(generations)
+        With use_graph the generation's launches (whose arguments never change:
+        gen and sigma live in the device GA state) are captured once in a HIP
+        graph and replayed."""
+        if self.use_graph:
+            if self.graph is None:
+                self.graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.graph):
+                    self._enqueue()
+            self.graph.replay()
+        else:
+            self._enqueue()
+
+    def _enqueue(self):
+        e, L, s = self.e, self.L, stream_ptr()
+        P, G, n_loc = self.P, self.G, self.n_loc
+        arl = self.arl
+        # 1. ask (models/model.py:65-71); in fast_step mode the previous
+        #    generation's ga_step already asked this one
+        if self.fast_step:
+            pass
+        elif self.torch_rng:
+            st_now = self.state.cpu().numpy().view(STATE_DTYPE)[0]
+            self.pop.copy_(_host_ask(self.master, float(st_now["sigma_mm"]), P))
+            if arl:
+                self.adv_pop.copy_(_host_ask(self.master_adv, float(st_now["sigma_adv"]), P))
+        else:
+            check(L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, e.seed, self.i0, n_loc,
+                                ptr(self.pop), G, s), "sgmm_ga_ask")
+            if arl:
+                check(L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, e.seed, self.i0,
+                                    n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
+        # 2. roll out the shard (drl_engine.py:104-115)
+        out, vout = self.out, self.vout
+        self.roll.fitness(self.ticks, self.train_eps, self.params, self.pop_loc, self.H, self.adv_loc, out=out)
+        if self.fused and self.val_eps is not None:
+            self.roll.fitness(self.ticks, self.val_eps, self.params, self.pop_loc, self.H, None, out=vout)
+        if self.fused and not arl:
+            tr_f, tr_t, va_f, va_t = out[0][:n_loc], out[1][:n_loc], out[0][n_loc:], out[1][n_loc:]
+        elif self.fused:
+            tr_f, tr_t, va_f, va_t = out[0], out[1], vout[0], vout[1]
+        else:
+            tr_f, tr_t, va_f, va_t = out[0], out[1], None, None
+        # 3. all-gather the shards' fitness (one collective per generation)
+        if self.world > 1:
+            tr_f, tr_t, va_f, va_t = _gather(self.gbuf, tr_f, tr_t, va_f, va_t, P, self.world, self.group)
+        if self.fast_step:
+            # 4+5+next ask: tell both evolvers, validation bookkeeping, ask gen+1
+            # (the next ask runs as its own many-workgroup kernel: one workgroup
+            # of Philox/Box-Muller is slower than a launch boundary)
+            check(L.sgmm_ga_step(ptr(self.state), ptr(tr_f), ptr(tr_t), ptr(va_f), ptr(va_t), P,
+                                 ptr(self.master), ptr(self.master_adv) if arl else None,
+                                 ptr(self.best_master), G, ADV_GENOME if arl else 0, e.seed,
+                                 ptr(self.hist), self.generations, None, None, self.i0, n_loc, s),
+                  "sgmm_ga_step")
+            check(L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, e.seed, self.i0, n_loc,
+                                ptr(self.pop), G, s), "sgmm_ga_ask")
+            if arl:
+                check(L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, e.seed, self.i0,
+                                    n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
+            return
+        # 4. tell both evolvers (model.py:73-76, drl_engine.py:119-125)
+        check(L.sgmm_ga_tell(ptr(self.state), ptr(tr_f), ptr(tr_t), P, ptr(self.master),
+                             ptr(self.pop) if self.torch_rng else None, G,
+                             ptr(self.master_adv) if arl else None,
+                             ptr(self.adv_pop) if (arl and self.torch_rng) else None, ADV_GENOME, G,
+                             ADV_GENOME if arl else 0, e.seed, ptr(self.hist), self.generations, s),
+              "sgmm_ga_tell")
+        # 5. validation of the best (drl_engine.py:129-171)
+        if not self.fused:
+            self.roll.fitness(self.ticks, self.val_eps, self.params, self.master.view(1, G), self.H, None,
+                              out=vout)
+            va_f, va_t = vout
+        check(L.sgmm_ga_val_update(ptr(self.state), ptr(va_f), ptr(va_t), 1 if self.fused else 0,
+                                   ptr(self.master), ptr(self.best_master), G, ptr(self.hist),
+                                   self.generations, s), "sgmm_ga_val_update")
+        if self.torch_rng:
+            TradingPolicy()  # the reference's validation builds a TradingPolicy() (RNG draw)
+
+    def flush(self, upto: int):
+        """History rows [emitted, upto) to the host: log lines, checkpoint."""
+        if upto <= self.emitted:
+            return
+        e = self.e
+        rows = self.hist[self.emitted:upto].cpu().numpy().view(HIST_DTYPE).reshape(-1)
+        improved_any = False
+        for k, r in enumerate(rows):
+            g = self.emitted + k
+            imp = bool(r["flags"] & 1)
+            improved_any |= imp
+            if r["flags"] & 2:
+                e._log(f">>> Sigma decayed to {r['sigma_after']:.4f} due to no improvement")
+            self.history["gen"].append(g)
+            self.history["train_f"].append(np.float64(r["train_f"]))
+            self.history["val_f"].append(np.float64(r["val_f"]))
+            self.history["train_trades"].append(int(r["train_trades"]))
+            self.history["val_trades"].append(int(r["val_trades"]))
+            if g % 5 == 0:
+                tag = "ARL:ON" if self.arl else "ARL:OFF"
+                e._log(f"Gen {g:03d} | {tag} | Best Train: {r['train_f']:.2f} | "
+                       f"Val: {r['val_f']:.2f}{'*' if imp else ''}")
+        if improved_any and self.rank == 0:
+            torch.save(genome_to_state_dict(self.best_master, self.H), self.best_path)
+        self.saved_any |= improved_any
+        self.emitted = upto
+
+    def finish(self):
+        """Flush, copy the evolver state back, reload the best-validation weights
+        (drl_engine.py:174-178); returns (master_policy, history)."""
+        e = self.e
+        self.ev1.record()
+        self.flush(self.generations)
         torch.cuda.synchronize()
-        self.timing = {"generations": generations, "ms": ev_start.elapsed_time(ev_end),
-                       "env_steps": generations * P * T_tr}
-        st = state.cpu().numpy().view(STATE_DTYPE)[0]
-        self.mm_evolver.sigma = float(st["sigma_mm"])
-        self.mm_evolver.master_policy.set_weights(master.cpu())
-        if arl:
-            self.adv_evolver.sigma = float(st["sigma_adv"])
-            self.adv_evolver.master_policy.set_weights(master_adv.cpu())
-        # reload the best-validation weights (drl_engine.py:174-176)
-        if saved_any:
-            self.mm_evolver.master_policy.load_state_dict(genome_to_state_dict(best_master, H))
-        elif os.path.exists(best_path):
-            self.mm_evolver.master_policy.load_state_dict(torch.load(best_path, weights_only=True))
-        return self.mm_evolver.master_policy, history
+        e.timing = {"generations": self.generations, "ms": self.ev0.elapsed_time(self.ev1),
+                    "env_steps": self.generations * self.P * self.T_tr}
+        st = self.state.cpu().numpy().view(STATE_DTYPE)[0]
+        e.mm_evolver.sigma = float(st["sigma_mm"])
+        e.mm_evolver.master_policy.set_weights(self.master.cpu())
+        if self.arl:
+            e.adv_evolver.sigma = float(st["sigma_adv"])
+            e.adv_evolver.master_policy.set_weights(self.master_adv.cpu())
+        if self.saved_any:
+            e.mm_evolver.master_policy.load_state_dict(genome_to_state_dict(self.best_master, self.H))
+        elif os.path.exists(self.best_path):
+            e.mm_evolver.master_policy.load_state_dict(torch.load(self.best_path, weights_only=True))
+        return e.mm_evolver.master_policy, self.history
 
 
 # ---------------------------------------------------------------------- small helpers
@@ -369,6 +455,7 @@ STATE_DTYPE = np.dtype([("sigma_mm", "<f8"), ("sigma_adv", "<f8"), ("best_val", 
                         ("improved", "<i4"), ("decayed", "<i4"), ("patience", "<i4"),
                         ("pad_", "<i4"), ("decay", "<f8")])
 assert HIST_DTYPE.itemsize == ctypes_size(GAHistory) and STATE_DTYPE.itemsize == ctypes_size(GAState)
+HIST_STATE_SIZES = (STATE_DTYPE.itemsize, HIST_DTYPE.itemsize)
 
 
 def _host_ask(master_dev, sigma, P):

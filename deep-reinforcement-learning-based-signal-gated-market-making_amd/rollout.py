@@ -148,10 +148,20 @@ class RolloutEngine:
         self.device = torch.device(device)
         self._ws = None
 
-    def workspace(self, eps: EpisodeBatch, arl: bool) -> torch.Tensor:
+    def workspace_bytes(self, eps: EpisodeBatch, arl: bool) -> int:
         ns = (eps.inv_max - eps.inv_min + 1) * (4 if arl else 1)
-        need = int(self.L.sgmm_rollout_workspace_size(eps.n, eps.total_steps, ns))
+        return int(self.L.sgmm_rollout_workspace_size(eps.n, eps.total_steps, ns))
+
+    def reserve(self, eps: EpisodeBatch, arl: bool):
+        """Grow the workspace for this batch now (never inside a graph capture:
+        a captured launch must not see its workspace reallocated later)."""
+        self.workspace(eps, arl)
+
+    def workspace(self, eps: EpisodeBatch, arl: bool) -> torch.Tensor:
+        need = self.workspace_bytes(eps, arl)
         if self._ws is None or self._ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("workspace growth during graph capture; call reserve() first")
             self._ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self._ws
 

@@ -153,15 +153,12 @@ int sgmm_rollout_trace(const sgmm_ticks *ticks, const sgmm_episodes *eps,
                        double *fitness, int32_t *trades, void *stream);
 
 /* NeuroEvolution.ask (models/model.py:65-71) on device:
- * out[i,k] = master[k] + z(seed, stream_id, gen, i0+i, k) * (float)(*sigma),
+ * out[i,k] = master[k] + z(seed, stream_id, gen, i0+i, k) * (float)sigma,
  * z ~ N(0,1) from Philox4x32-10 + Box-Muller (counter-based, so any rank can
- * regenerate any individual).  sigma is a DEVICE pointer (the evolver's
- * sigma lives in sgmm_ga_state and decays on device).  out row stride
- * out_stride. */
-int sgmm_ga_ask(const float *master, int64_t n_params, const double *sigma,
-                uint64_t seed, uint32_t stream_id, uint32_t gen, int32_t i0, int32_t n,
-                float *out, int64_t out_stride, void *stream);
-
+ * regenerate any individual).  sigma and gen are read ON DEVICE from `state`
+ * (stream_id 0: sigma_mm, 1: sigma_adv; gen = state->gen), so a generation's
+ * launches have fixed arguments and can be captured once in a HIP graph and
+ * replayed.  out row stride out_stride. */
 /* Device GA bookkeeping state (DRLEngine.train locals, drl_engine.py:84-89,
  * 143-160).  Initialise with sgmm_ga_state_init. */
 typedef struct sgmm_ga_state {
@@ -195,28 +192,58 @@ typedef struct sgmm_ga_history {
 int sgmm_ga_state_init(sgmm_ga_state *state, double sigma, int32_t patience, double decay,
                        void *stream);
 
+int sgmm_ga_ask(const float *master, int64_t n_params, const sgmm_ga_state *state,
+                uint32_t stream_id, uint64_t seed, int32_t i0, int32_t n,
+                float *out, int64_t out_stride, void *stream);
+
 /* NeuroEvolution.tell for both evolvers (model.py:73-76, drl_engine.py:119-125):
  * best = first index of max(fitness) (np.argmax; NaN counts as max),
  * adv_best = first index of max(-fitness).  The new master rows are written
  * into master_mm / master_adv either by copying row best of `pop_mm` /
  * `pop_adv` (host-supplied populations, may be NULL) or, when the pop
  * pointer is NULL, by regenerating the ask() of that index in place
- * (same seed/stream/gen as the ask).  P = global population size. */
+ * (same seed/stream/gen as the ask).  P = global population size.
+ * history: array of history_cap rows; row state->gen is written. */
 int sgmm_ga_tell(sgmm_ga_state *state, const double *fitness, const int32_t *trades, int32_t P,
                  float *master_mm, const float *pop_mm, int64_t pop_mm_stride,
                  float *master_adv, const float *pop_adv, int64_t pop_adv_stride,
-                 int64_t n_params_mm, int64_t n_params_adv,
-                 uint64_t seed, uint32_t gen, sgmm_ga_history *history_row, void *stream);
+                 int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
+                 sgmm_ga_history *history, int32_t history_cap, void *stream);
 
 /* Validation bookkeeping after the best individual's validation rollout
  * (drl_engine.py:129-171): val_fitness/val_trades are read at index
- * val_index (the best of this generation when val was evaluated for the
- * whole population, or 0).  On improvement master_mm is copied to
- * best_master (the checkpoint slot).  Applies sigma decay. */
+ * state->best_idx when use_best_index (validation evaluated for the whole
+ * population), else at 0.  On improvement master_mm is copied to best_master
+ * (the checkpoint slot).  Applies sigma decay, completes history row
+ * state->gen, then advances state->gen. */
 int sgmm_ga_val_update(sgmm_ga_state *state, const double *val_fitness,
                        const int32_t *val_trades, int32_t use_best_index,
                        const float *master_mm, float *best_master, int64_t n_params_mm,
-                       sgmm_ga_history *history_row, void *stream);
+                       sgmm_ga_history *history, int32_t history_cap, void *stream);
+
+/* One generation boundary in a single launch (single process or after the
+ * fitness all-gather): tell (as sgmm_ga_tell, masters regenerated in place),
+ * validation bookkeeping with the validation fitness of the whole population
+ * (as sgmm_ga_val_update with use_best_index), then -- if next_pop_mm is not
+ * NULL -- the ask() of the NEXT generation for individuals [i0, i0+n) with the
+ * updated sigma (as sgmm_ga_ask; next_pop_adv likewise when master_adv).
+ * Meant for modest P * n_params (one workgroup); use the separate entry points
+ * for large populations. */
+int sgmm_ga_step(sgmm_ga_state *state, const double *fitness, const int32_t *trades,
+                 const double *val_fitness, const int32_t *val_trades, int32_t P,
+                 float *master_mm, float *master_adv, float *best_master,
+                 int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
+                 sgmm_ga_history *history, int32_t history_cap,
+                 float *next_pop_mm, float *next_pop_adv, int32_t i0, int32_t n, void *stream);
+
+/* Kernel timing for benchmarks / diagnostics (not on by default).
+ * While enabled, every kernel the library launches is bracketed by a pair of
+ * hipEvents recorded on its stream.  sgmm_profile_read waits for the recorded
+ * events, writes up to max_kinds entries (name[i] = names + 48*i,
+ * NUL-terminated; total_ms[i]; count[i]) and clears the record.  Returns the
+ * number of kernel kinds written, or < 0 on error. */
+int sgmm_profile_enable(int enable);
+int sgmm_profile_read(int max_kinds, char *names, double *total_ms, int64_t *count);
 
 #ifdef __cplusplus
 }

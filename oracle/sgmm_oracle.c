@@ -67,7 +67,17 @@ static int32_t act_to_int(float r)
     return (int32_t)r;
 }
 
-static float relu32(float a) { return a < 0.0f ? 0.0f : a; }
+/* ReLU on the bit pattern, max(bits, 0) as int32 -- the kernels' v_max_i32.
+ * Identical to torch's relu for every non-NaN input; NaN pre-activations
+ * (only NaN state inputs produce them) are outside the parity domain. */
+static float relu32(float a)
+{
+    int32_t b;
+    memcpy(&b, &a, sizeof b);
+    b = b > 0 ? b : 0;
+    memcpy(&a, &b, sizeof a);
+    return a;
+}
 
 /* ---- FTPEnv.step (Env/market_env.py:22-67) -------------------------------- */
 /* out4 = {reward, pnl_reward, inventory_reward, fee_paid}; fills = {buy, sell} */

@@ -1,0 +1,69 @@
+"""CPU checks of the C ABI boundary: libsgmm.so loads without a GPU and
+exports exactly the functions include/sgmm.h declares; ctypes mirrors of the
+ABI structs have the header's sizes/offsets."""
+import ctypes
+import re
+import subprocess
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "sgmm.h"
+
+
+def declared_functions():
+    text = HEADER.read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(sgmm_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for must in ("sgmm_rollout_fitness", "sgmm_rollout_trace", "sgmm_env_step_batch",
+                 "sgmm_policy_forward", "sgmm_ga_ask", "sgmm_ga_tell", "sgmm_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(sgmm):
+    from sgmm_amd import _lib
+    L = _lib.load()
+    lib_path = _lib.LIB_PATH
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(lib_path)], capture_output=True, text=True,
+                        check=True).stdout
+    exported = set(re.findall(r" T (sgmm_[a-z_0-9]+)", nm))
+    declared = set(declared_functions())
+    assert declared <= exported, declared - exported
+    assert exported <= declared, exported - declared  # nothing undocumented
+    assert set(_lib.SIGNATURES) == declared            # the binding covers the header
+    assert L.sgmm_abi_version() == 1
+
+
+def test_struct_layouts_match_header(sgmm):
+    from sgmm_amd import _lib
+    assert ctypes.sizeof(_lib.EnvParams) == 48
+    assert ctypes.sizeof(_lib.GAState) == 80 and _lib.GAState.decay.offset == 72
+    assert ctypes.sizeof(_lib.GAHistory) == 40
+    assert _lib.Episodes.genome.offset == 24 and ctypes.sizeof(_lib.Episodes) == 72
+    assert ctypes.sizeof(_lib.Ticks) == 56
+
+
+def test_argument_errors_need_no_gpu(sgmm):
+    """Validation happens before any HIP call: bad arguments fail cleanly on CPU."""
+    from sgmm_amd import _lib
+    L = _lib.load()
+    rc = L.sgmm_policy_forward(None, 0, 16, None, None, None, 10, None)
+    assert rc == -1 and b"null" in L.sgmm_last_error()
+    rc = L.sgmm_policy_forward(ctypes.c_void_p(8), 370, 12, None, ctypes.c_void_p(8), ctypes.c_void_p(8), 1, None)
+    assert rc == -1 and b"hidden" in L.sgmm_last_error()
+    # no adversary: u32 prefix words + u32 chunk maps + f64 rewards, 256-aligned sections
+    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == 4096 + 256 + 40192
+    # adversary (20 states): u64 fill words + f64 rewards
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 160000
+
+
+def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        sgmm.RolloutEngine("cuda")

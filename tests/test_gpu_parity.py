@@ -235,3 +235,17 @@ def test_dropin_evaluate_individual(golden, sgmm):
                                         torch.from_numpy(ep["adv"]), bundle, ep["phi"], ep["tick"],
                                         ep["fee"], st, use_arl=ep["adv"] is not None)
         assert f == ep["fitness"] and t == ep["trades"]
+
+
+@pytest.mark.parametrize("path", ["valu", "mfma"])
+def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
+    """The f32-MFMA and the VALU table kernels both reproduce the oracle's
+    canonical fma chains bit for bit (the MFMA k-order equals the chain)."""
+    monkeypatch.setenv("SGMM_TABLE_PATH", path)
+    eps = list(episodes_from_fixture(golden("g2_synthetic.npz")))
+    eps += _synthetic_batch(sgmm, 4, 1000, 32, seed=77, sigma=0.4)
+    for (H, arl), group in _groups(eps).items():
+        (fit, trd), _ = _run_batch(sgmm, group, arl)
+        for i, ep in enumerate(group):
+            f, t = _oracle_eval(oracle, ep)
+            assert trd[i].item() == t and fit[i].item() == f, (path, H, arl, i)
