@@ -3,8 +3,8 @@
 Drop-in for the hot path of KAS-W/Deep-Reinforcement-Learning-Based-Signal-
 Gated-Market-Making: FTPEnv (Env/market_env.py), TradingPolicy /
 AdversaryPolicy / NeuroEvolution (models/model.py), evaluate_individual /
-DRLEngine (Env/drl_engine.py) and run_agent_training_pipeline
-(pipeline/agent_trainer.py).  Compute runs in libsgmm.so (HIP, gfx950).
+DRLEngine (Env/drl_engine.py); pipeline/agent_trainer.py then runs unchanged
+on top of them (see dropin/ and INTEGRATION.md).  Compute runs in libsgmm.so (HIP, gfx950).
 
 The directory name carries hyphens, so import it through the repository's
 ``sgmm_pkg.load()`` (registers it as ``sgmm_amd``), or put ``dropin/`` on

@@ -7,22 +7,23 @@
 //
 // Fitness path (sgmm_rollout_fitness) -- two kernels:
 //
-//  1. k_policy_table: the inventory feedback makes an episode a serial chain,
+//  1. policy table: the inventory feedback makes an episode a serial chain,
 //     but the policy only sees (signal_t, inventory) and the inventory takes
 //     at most 8 values (caps +-2 -> 5).  So the policy, the FPT fill test and
 //     the reward are evaluated for EVERY (tick, inventory[, adversary flags])
-//     state in parallel: one lane per tick, weights wave-uniform (scalar
-//     loads), the fp32 MLP on the VALU (the f32 MFMA rate equals the VALU rate
-//     on gfx950 and the 3->H->H->2 shapes pad badly onto 16x16x4 tiles, so
-//     MFMA would add work, not speed).  Output per tick: 2 fill bits per state
-//     (u64) and one float64 reward per state.
+//     state in parallel.  H >= 16: k_policy_table_mfma, the two H-wide layers
+//     on v_mfma_f32_16x16x4_f32 (whose k-ordered fused chain IS the canonical
+//     dot-product order); H = 8 or SGMM_TABLE_PATH=valu: k_policy_table, one
+//     lane per (tick, state) on the VALU.  Output per tick: the exclusive
+//     prefix transition map of its 64-tick chunk (+ traded mask) and one
+//     float64 reward per state; per chunk: the chunk's full map.  With the
+//     adversary: 2 fill bits per (inventory, previous fills) state (u64).
 //
-//  2. k_path_scan (one workgroup per episode): chunked parallel walk of the
-//     5-state (20 with the adversary) transducer -- every chunk of 64 ticks is
-//     walked from every start state, the chunk end-maps are chained, each
-//     chunk is replayed from its true start -- and the selected rewards are
-//     summed in the reference's sequential float64 order (bit-exact), trades
-//     counted with a block reduction.
+//  2. path scan (one workgroup per episode): chunk start states from a scan
+//     of the chunk maps, each tick's state = one field of its prefix word, the
+//     selected rewards summed in the reference's sequential float64 order
+//     (bit-exact), trades counted with a block reduction.  The adversary
+//     variant walks the 20-state transducer chunk by chunk.
 //
 // Trace path (sgmm_rollout_trace): k_rollout_direct, one wave per episode,
 // lane = hidden neuron, the literal step loop (independent second

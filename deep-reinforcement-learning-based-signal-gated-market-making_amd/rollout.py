@@ -207,7 +207,7 @@ class RolloutEngine:
 
 def policy_forward(genomes: torch.Tensor, hidden: int, states: torch.Tensor,
                    genome_idx: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """Batched TradingPolicy forward on device (models/model.py:267-269)."""
+    """Batched TradingPolicy forward on device (models/model.py:24-26)."""
     L = _lib.load()
     out = torch.empty((states.shape[0], 2), dtype=torch.float32, device=states.device)
     rc = L.sgmm_policy_forward(ptr(genomes), genomes.stride(0), hidden, ptr(genome_idx),
@@ -218,7 +218,7 @@ def policy_forward(genomes: torch.Tensor, hidden: int, states: torch.Tensor,
 
 def adversary_forward(genomes: torch.Tensor, states: torch.Tensor,
                       genome_idx: torch.Tensor | None = None, stream=None) -> torch.Tensor:
-    """Batched AdversaryPolicy forward on device (models/model.py:292-293)."""
+    """Batched AdversaryPolicy forward on device (models/model.py:49-50)."""
     L = _lib.load()
     out = torch.empty((states.shape[0], 2), dtype=torch.float32, device=states.device)
     rc = L.sgmm_adversary_forward(ptr(genomes), genomes.stride(0), ptr(genome_idx),

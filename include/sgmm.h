@@ -107,7 +107,7 @@ int sgmm_env_step_batch(const sgmm_env_params *params, const int32_t *param_idx,
                         double *fee_paid, uint8_t *fill_buy, uint8_t *fill_sell,
                         int64_t n, void *stream);
 
-/* Batched TradingPolicy.forward (models/model.py:267-269): out[i] =
+/* Batched TradingPolicy.forward (models/model.py:24-26): out[i] =
  * MLP(genomes[genome_idx[i]], states[i]).  Genome layout = parameters()
  * order W1[H,3] b1[H] W2[H,H] b2[H] W3[2,H] b3[2] (H*H+7H+2 floats).
  * genome_idx may be NULL (row i).  hidden in {8,16,32,64}. */
@@ -115,8 +115,8 @@ int sgmm_policy_forward(const float *genomes, int64_t genome_stride, int32_t hid
                         const int32_t *genome_idx, const float *states, float *out,
                         int64_t n, void *stream);
 
-/* Batched AdversaryPolicy.forward (models/model.py:292-293): tanh outputs,
- * weights = the first 74 floats of each genome row (model.py:295-300). */
+/* Batched AdversaryPolicy.forward (models/model.py:49-50): tanh outputs,
+ * weights = the first 74 floats of each genome row (model.py:52-57). */
 int sgmm_adversary_forward(const float *genomes, int64_t genome_stride,
                            const int32_t *genome_idx, const float *states, float *out,
                            int64_t n, void *stream);
