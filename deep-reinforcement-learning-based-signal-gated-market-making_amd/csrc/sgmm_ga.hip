@@ -195,13 +195,28 @@ __global__ void k_ga_state_init(sgmm_ga_state* st, double sigma, int32_t patienc
 constexpr int kStepBlock = 1024;
 constexpr int kMaxStepParams = 4096;  // master staged in LDS
 
-__device__ void block_argmax2(const double* __restrict__ fit, int P, int& best, int& abest,
-                              double* sv, int* si) {
+// Population results gathered shard by shard: individual i's value lives in
+// shard i / n at byte offset (i / n) * stride, element i % n (n <= 0: one
+// contiguous array).  This is the layout of an all-gather of per-rank records.
+struct ShardView {
+    int32_t n;
+    int64_t stride;
+};
+
+template <class T>
+__device__ __forceinline__ T shard_at(const T* __restrict__ base, ShardView v, int i) {
+    if (v.n <= 0) return base[i];
+    const char* p = reinterpret_cast<const char*>(base) + (int64_t)(i / v.n) * v.stride;
+    return reinterpret_cast<const T*>(p)[i % v.n];
+}
+
+__device__ void block_argmax2(const double* __restrict__ fit, ShardView sv_, int P, int& best,
+                              int& abest, double* sv, int* si) {
     const int tid = threadIdx.x, nt = blockDim.x;
     double bv = 0.0, av = 0.0;
     int bi = -1, aj = -1;
     for (int i = tid; i < P; i += nt) {
-        const double f = fit[i];
+        const double f = shard_at(fit, sv_, i);
         if (bi < 0 || better(f, i, bv, bi)) { bv = f; bi = i; }
         if (aj < 0 || better(-f, i, av, aj)) { av = -f; aj = i; }
     }
@@ -257,7 +272,7 @@ __device__ void ask_rows(const float* lds_master, int64_t n, float sig, uint64_t
 __global__ __launch_bounds__(kStepBlock) void k_ga_step(
     sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
     const int32_t* __restrict__ trades, const double* __restrict__ vfit,
-    const int32_t* __restrict__ vtrades, int32_t P, float* __restrict__ master,
+    const int32_t* __restrict__ vtrades, int32_t P, ShardView shard, float* __restrict__ master,
     float* __restrict__ master_adv, float* __restrict__ best_master, int64_t n_mm, int64_t n_adv,
     uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap,
     float* __restrict__ next_mm, float* __restrict__ next_adv, int32_t i0, int32_t n) {
@@ -271,7 +286,7 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
     const uint32_t gen = (uint32_t)st->gen;
     sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
     int best, abest;
-    block_argmax2(fit, P, best, abest, sv, si);
+    block_argmax2(fit, shard, P, best, abest, sv, si);
     const float sig_mm = (float)st->sigma_mm, sig_adv = (float)st->sigma_adv;
     __syncthreads();
     // tell (model.py:73-76; drl_engine.py:119-125)
@@ -279,7 +294,7 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
     if (master_adv) regen_master(master_adv, la, n_adv, sig_adv, seed, 1u, gen, abest);
     if (tid == 0) {
         // validation of the best (drl_engine.py:129-171)
-        const double v = vfit[best];
+        const double v = shard_at(vfit, shard, best);
         improved = v > st->best_val;
         int decayed = 0;
         if (improved) {
@@ -296,7 +311,7 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
         }
         st->best_idx = best;
         st->adv_best_idx = abest;
-        st->last_train_f = fit[best];
+        st->last_train_f = shard_at(fit, shard, best);
         st->improved = improved;
         st->decayed = decayed;
         st->last_val_f = v;
@@ -304,11 +319,11 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
         next_sig[0] = (float)st->sigma_mm;
         next_sig[1] = (float)st->sigma_adv;
         if (hist) {
-            hist->train_f = fit[best];
-            hist->train_trades = trades ? trades[best] : 0;
+            hist->train_f = shard_at(fit, shard, best);
+            hist->train_trades = trades ? shard_at(trades, shard, best) : 0;
             hist->best_idx = best;
             hist->val_f = v;
-            hist->val_trades = vtrades ? vtrades[best] : 0;
+            hist->val_trades = vtrades ? shard_at(vtrades, shard, best) : 0;
             hist->sigma_after = st->sigma_mm;
             hist->flags = improved | (decayed << 1);
         }
@@ -327,7 +342,7 @@ using namespace sgmm;
 
 extern "C" int sgmm_ga_step(sgmm_ga_state* state, const double* fitness, const int32_t* trades,
                             const double* val_fitness, const int32_t* val_trades, int32_t P,
-                            float* master_mm, float* master_adv, float* best_master,
+                            int32_t shard_n, int64_t shard_stride, float* master_mm, float* master_adv, float* best_master,
                             int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
                             sgmm_ga_history* history, int32_t history_cap, float* next_pop_mm,
                             float* next_pop_adv, int32_t i0, int32_t n, void* stream) {
@@ -336,9 +351,11 @@ extern "C" int sgmm_ga_step(sgmm_ga_state* state, const double* fitness, const i
     SGMM_REQUIRE(P > 0 && n_params_mm > 0 && n_params_mm <= kMaxStepParams, "bad P / n_params_mm");
     SGMM_REQUIRE(!master_adv || (n_params_adv > 0 && n_params_adv <= kMaxStepParams), "n_params_adv");
     SGMM_REQUIRE(!next_pop_mm || (n >= 0 && i0 >= 0), "bad next-ask shard");
+    SGMM_REQUIRE(shard_n <= 0 || shard_stride >= 8LL * shard_n, "shard_stride < 8 * shard_n");
     ProfScope prof("ga_step", as_stream(stream));
     hipLaunchKernelGGL(k_ga_step, dim3(1), dim3(kStepBlock), 0, as_stream(stream), state,
-                       fitness, trades, val_fitness, val_trades, P, master_mm, master_adv,
+                       fitness, trades, val_fitness, val_trades, P, ShardView{shard_n, shard_stride},
+                       master_mm, master_adv,
                        best_master, n_params_mm, n_params_adv, seed, history, history_cap,
                        next_pop_mm, next_pop_adv, i0, n);
     SGMM_LAUNCHED();

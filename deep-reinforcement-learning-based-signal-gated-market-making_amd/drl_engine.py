@@ -25,6 +25,7 @@ from . import _lib
 from ._lib import GAHistory, GAState, check, ptr, stream_ptr
 from .model import NeuroEvolution, TradingPolicy, genome_size, genome_to_state_dict, hidden_from_genome
 from .rollout import EnvConfig, EpisodeBatch, RolloutEngine, TickStore, params_tensor
+from .shard import FitnessRecords, shard_bounds, shard_capacity  # noqa: F401 (re-exported)
 
 ADV_GENOME = genome_size(32)  # adversary evolver masters are TradingPolicy() genomes (model.py:63)
 
@@ -124,13 +125,6 @@ def _dist_info(dist):
         g = dist if dist not in (None, True) else None
         return g, torch.distributed.get_rank(g), torch.distributed.get_world_size(g)
     return None, 0, 1
-
-
-def shard_bounds(P, rank, world):
-    """Contiguous population shard of a rank: [i0, i1)."""
-    base, rem = divmod(P, world)
-    i0 = rank * base + min(rank, rem)
-    return i0, i0 + base + (1 if rank < rem else 0)
 
 
 class DRLEngine:
@@ -234,8 +228,9 @@ class TrainingSession:
         G = self.G
         self.i0, self.i1 = shard_bounds(P, self.rank, self.world)
         n_loc = self.n_loc = self.i1 - self.i0
+        n_cap = self.n_cap = shard_capacity(P, self.world)  # record slots per rank
         arl = self.arl = eng.use_arl
-        self.fused = eng.val_mode == "fused" or (eng.val_mode == "auto" and n_loc <= 512)
+        self.fused = eng.val_mode == "fused" or (eng.val_mode == "auto" and n_cap <= 512)
         self.torch_rng = eng.rng == "torch"
         self.generations = int(generations)
         # (rng="torch" with world > 1: every rank draws the identical full
@@ -244,37 +239,48 @@ class TrainingSession:
         (tr_off, self.T_tr), (va_off, self.T_va) = self.ticks.segments
         self.params = params_tensor([EnvConfig(phi=eng.phi, tick_size=eng.tick_size,
                                                fee_rate=eng.fee_rate)], dev)
+        # episode slots follow the record layout: n_cap per phase, the shard's
+        # n_loc individuals first, then zero-length pads (never read back)
+        pad = n_cap - n_loc
+
+        def phase(off, T):
+            return (np.concatenate([np.arange(n_loc), np.zeros(pad, np.int64)]),
+                    np.full(n_cap, off), np.concatenate([np.full(n_loc, T), np.zeros(pad, np.int64)]))
+
+        g_tr, o_tr, l_tr = phase(tr_off, self.T_tr)
+        g_va, o_va, l_va = phase(va_off, self.T_va)
+        self.rec = FitnessRecords(P, self.world, dev)
         if self.fused and not arl:  # one launch: training + validation episodes of the shard
-            self.train_eps = EpisodeBatch(
-                np.concatenate([np.arange(n_loc), np.arange(n_loc)]),
-                np.concatenate([np.full(n_loc, tr_off), np.full(n_loc, va_off)]),
-                np.concatenate([np.full(n_loc, self.T_tr), np.full(n_loc, self.T_va)]),
-                np.zeros(2 * n_loc)).to(dev)
+            self.train_eps = EpisodeBatch(np.concatenate([g_tr, g_va]), np.concatenate([o_tr, o_va]),
+                                          np.concatenate([l_tr, l_va]), np.zeros(2 * n_cap)).to(dev)
             self.val_eps = None
+            self.out, self.vout = self.rec.both, None
         else:
-            self.train_eps = EpisodeBatch(np.arange(n_loc), np.full(n_loc, tr_off), np.full(n_loc, self.T_tr),
-                                          np.zeros(n_loc), adv=np.arange(n_loc) if arl else None).to(dev)
-            nv = n_loc if self.fused else 1
-            self.val_eps = EpisodeBatch(np.arange(nv), np.full(nv, va_off), np.full(nv, self.T_va),
-                                        np.zeros(nv)).to(dev)
+            self.train_eps = EpisodeBatch(g_tr, o_tr, l_tr, np.zeros(n_cap),
+                                          adv=g_tr if arl else None).to(dev)
+            self.out = self.rec.train
+            if self.fused:
+                self.val_eps = EpisodeBatch(g_va, o_va, l_va, np.zeros(n_cap)).to(dev)
+                self.vout = self.rec.val
+            else:  # validation of the best only (reference order)
+                self.val_eps = EpisodeBatch(np.zeros(1), np.full(1, va_off), np.full(1, self.T_va),
+                                            np.zeros(1)).to(dev)
+                self.vout = (torch.empty(1, dtype=torch.float64, device=dev),
+                             torch.empty(1, dtype=torch.int32, device=dev))
         f32 = dict(dtype=torch.float32, device=dev)
-        n_pop = P if self.torch_rng else n_loc
-        self.pop = torch.empty((n_pop, G), **f32)
-        self.pop_loc = self.pop[self.i0:self.i1] if self.torch_rng else self.pop
-        self.adv_pop = torch.empty((n_pop, ADV_GENOME), **f32) if arl else None
-        self.adv_loc = (self.adv_pop[self.i0:self.i1] if self.torch_rng else self.adv_pop) if arl else None
+        # population rows: the full population when the host draws it (torch
+        # RNG), else the shard's capacity (pads point at row 0, which exists)
+        n_rows = P if self.torch_rng else max(n_cap, 1)
+        self.pop = torch.empty((n_rows, G), **f32)
+        lo = min(self.i0, P - 1)
+        self.pop_loc = self.pop[lo:lo + max(n_cap, 1)] if self.torch_rng else self.pop
+        self.adv_pop = torch.empty((n_rows, ADV_GENOME), **f32) if arl else None
+        self.adv_loc = (self.adv_pop[lo:lo + max(n_cap, 1)] if self.torch_rng else self.adv_pop) if arl else None
         self.master = eng.mm_evolver.master_policy.get_weights().to(**f32)
         self.master_adv = eng.adv_evolver.master_policy.get_weights().to(**f32) if arl else None
         self.best_master = torch.zeros(G, **f32)
         self.state = torch.zeros(HIST_STATE_SIZES[0], dtype=torch.uint8, device=dev)
         self.hist = torch.zeros((self.generations, HIST_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-        self.out = (torch.empty(self.train_eps.n, dtype=torch.float64, device=dev),
-                    torch.empty(self.train_eps.n, dtype=torch.int32, device=dev))
-        self.vout = (torch.empty(self.val_eps.n, dtype=torch.float64, device=dev),
-                     torch.empty(self.val_eps.n, dtype=torch.int32, device=dev)) if self.val_eps else None
-        n_max = shard_bounds(P, 0, self.world)[1]
-        self.gbuf = torch.empty((self.world, 4, n_max), dtype=torch.float64, device=dev) \
-            if self.world > 1 else None
         if arl and eng.adv_evolver.sigma != eng.mm_evolver.sigma:
             raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
         check(self.L.sgmm_ga_state_init(ptr(self.state), float(eng.mm_evolver.sigma), eng.patience,
@@ -282,18 +288,14 @@ class TrainingSession:
         # generation boundary in one launch (tell + validation + next ask) when the
         # population is drawn on device and validated in the training launch
         self.fast_step = (not self.torch_rng and self.fused and G <= 4096 and ADV_GENOME <= 4096
-                          and n_loc * G <= (1 << 22))
-        if self.fast_step:  # the ask of generation 0; later asks happen inside ga_step
-            check(self.L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, eng.seed, self.i0, n_loc,
-                                     ptr(self.pop), G, stream_ptr()), "sgmm_ga_ask")
-            if arl:
-                check(self.L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, eng.seed,
-                                         self.i0, n_loc, ptr(self.adv_pop), ADV_GENOME, stream_ptr()),
-                      "sgmm_ga_ask(adv)")
-        # one generation = fixed launches -> replayable graph (eager when the host
-        # draws the population or a collective sits inside the generation)
-        self.use_graph = bool(eng.use_graph) and not self.torch_rng and self.world == 1
-        self.graph = None
+                          and n_cap * G <= (1 << 22))
+        if self.fast_step:  # the ask of generation 0; later asks follow each ga_step
+            self._ask()
+        # one generation = fixed launches -> replayable HIP graphs: the whole
+        # generation on one rank; with several ranks the rollout and the boundary
+        # are captured separately around the (eager) all-gather
+        self.use_graph = bool(eng.use_graph) and not self.torch_rng
+        self.graphs = None
         self.roll.reserve(self.train_eps, arl)
         if self.val_eps is not None:
             self.roll.reserve(self.val_eps, False)
@@ -309,77 +311,86 @@ class TrainingSession:
         """Enqueue generation ``gen`` (drl_engine.py:92-171) on the current stream.
 
         With use_graph the generation's launches (whose arguments never change:
-        gen and sigma live in the device GA state) are captured once in a HIP
-        graph and replayed."""
-        if self.use_graph:
-            if self.graph is None:
-                self.graph = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(self.graph):
-                    self._enqueue()
-            self.graph.replay()
-        else:
-            self._enqueue()
+        gen and sigma live in the device GA state) are captured once in HIP
+        graphs and replayed."""
+        if not self.use_graph:
+            self._rollout()
+            self._exchange()
+            self._boundary()
+            return
+        if self.graphs is None:
+            self.graphs = []
+            phases = [(self._rollout, self._boundary)] if self.world == 1 else [(self._rollout,), (self._boundary,)]
+            for fns in phases:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for f in fns:
+                        f()
+                self.graphs.append(g)
+        self.graphs[0].replay()
+        if self.world > 1:
+            self._exchange()
+            self.graphs[1].replay()
 
-    def _enqueue(self):
-        e, L, s = self.e, self.L, stream_ptr()
-        P, G, n_loc = self.P, self.G, self.n_loc
-        arl = self.arl
-        # 1. ask (models/model.py:65-71); in fast_step mode the previous
-        #    generation's ga_step already asked this one
-        if self.fast_step:
-            pass
-        elif self.torch_rng:
+    def _ask(self):
+        """ask() of the shard (models/model.py:65-71) from the device master/sigma."""
+        e, L, s, G = self.e, self.L, stream_ptr(), self.G
+        check(L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, e.seed, self.i0, self.n_loc,
+                            ptr(self.pop), G, s), "sgmm_ga_ask")
+        if self.arl:
+            check(L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, e.seed, self.i0,
+                                self.n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
+
+    def _rollout(self):
+        """ask (unless the previous boundary did) + the shard's rollouts
+        (drl_engine.py:104-115, plus the fused validation episodes)."""
+        P = self.P
+        if self.torch_rng:
             st_now = self.state.cpu().numpy().view(STATE_DTYPE)[0]
             self.pop.copy_(_host_ask(self.master, float(st_now["sigma_mm"]), P))
-            if arl:
+            if self.arl:
                 self.adv_pop.copy_(_host_ask(self.master_adv, float(st_now["sigma_adv"]), P))
-        else:
-            check(L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, e.seed, self.i0, n_loc,
-                                ptr(self.pop), G, s), "sgmm_ga_ask")
-            if arl:
-                check(L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, e.seed, self.i0,
-                                    n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
-        # 2. roll out the shard (drl_engine.py:104-115)
-        out, vout = self.out, self.vout
-        self.roll.fitness(self.ticks, self.train_eps, self.params, self.pop_loc, self.H, self.adv_loc, out=out)
+        elif not self.fast_step:
+            self._ask()
+        self.roll.fitness(self.ticks, self.train_eps, self.params, self.pop_loc, self.H, self.adv_loc,
+                          out=self.out)
         if self.fused and self.val_eps is not None:
-            self.roll.fitness(self.ticks, self.val_eps, self.params, self.pop_loc, self.H, None, out=vout)
-        if self.fused and not arl:
-            tr_f, tr_t, va_f, va_t = out[0][:n_loc], out[1][:n_loc], out[0][n_loc:], out[1][n_loc:]
-        elif self.fused:
-            tr_f, tr_t, va_f, va_t = out[0], out[1], vout[0], vout[1]
-        else:
-            tr_f, tr_t, va_f, va_t = out[0], out[1], None, None
-        # 3. all-gather the shards' fitness (one collective per generation)
+            self.roll.fitness(self.ticks, self.val_eps, self.params, self.pop_loc, self.H, None, out=self.vout)
+
+    def _exchange(self):
+        """The generation's one collective: all-gather the per-rank records."""
         if self.world > 1:
-            tr_f, tr_t, va_f, va_t = _gather(self.gbuf, tr_f, tr_t, va_f, va_t, P, self.world, self.group)
+            self.rec.all_gather(self.group)
+
+    def _boundary(self):
+        """tell both evolvers, validation bookkeeping, sigma decay, next ask."""
+        e, L, s = self.e, self.L, stream_ptr()
+        P, G = self.P, self.G
+        arl = self.arl
         if self.fast_step:
-            # 4+5+next ask: tell both evolvers, validation bookkeeping, ask gen+1
-            # (the next ask runs as its own many-workgroup kernel: one workgroup
-            # of Philox/Box-Muller is slower than a launch boundary)
-            check(L.sgmm_ga_step(ptr(self.state), ptr(tr_f), ptr(tr_t), ptr(va_f), ptr(va_t), P,
+            # tell + validation + sigma decay in one launch on the gathered
+            # records; the next ask runs as its own many-workgroup kernel (one
+            # workgroup of Philox/Box-Muller is slower than a launch boundary)
+            check(L.sgmm_ga_step(ptr(self.state), *self.rec.step_args(),
                                  ptr(self.master), ptr(self.master_adv) if arl else None,
                                  ptr(self.best_master), G, ADV_GENOME if arl else 0, e.seed,
-                                 ptr(self.hist), self.generations, None, None, self.i0, n_loc, s),
+                                 ptr(self.hist), self.generations, None, None, self.i0, self.n_loc, s),
                   "sgmm_ga_step")
-            check(L.sgmm_ga_ask(ptr(self.master), G, ptr(self.state), 0, e.seed, self.i0, n_loc,
-                                ptr(self.pop), G, s), "sgmm_ga_ask")
-            if arl:
-                check(L.sgmm_ga_ask(ptr(self.master_adv), ADV_GENOME, ptr(self.state), 1, e.seed, self.i0,
-                                    n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
+            self._ask()
             return
-        # 4. tell both evolvers (model.py:73-76, drl_engine.py:119-125)
+        tr_f, tr_t, va_f, va_t = self.rec.population()
+        # tell both evolvers (model.py:73-76, drl_engine.py:119-125)
         check(L.sgmm_ga_tell(ptr(self.state), ptr(tr_f), ptr(tr_t), P, ptr(self.master),
                              ptr(self.pop) if self.torch_rng else None, G,
                              ptr(self.master_adv) if arl else None,
                              ptr(self.adv_pop) if (arl and self.torch_rng) else None, ADV_GENOME, G,
                              ADV_GENOME if arl else 0, e.seed, ptr(self.hist), self.generations, s),
               "sgmm_ga_tell")
-        # 5. validation of the best (drl_engine.py:129-171)
+        # validation of the best (drl_engine.py:129-171)
         if not self.fused:
             self.roll.fitness(self.ticks, self.val_eps, self.params, self.master.view(1, G), self.H, None,
-                              out=vout)
-            va_f, va_t = vout
+                              out=self.vout)
+            va_f, va_t = self.vout
         check(L.sgmm_ga_val_update(ptr(self.state), ptr(va_f), ptr(va_t), 1 if self.fused else 0,
                                    ptr(self.master), ptr(self.best_master), G, ptr(self.hist),
                                    self.generations, s), "sgmm_ga_val_update")
@@ -462,21 +473,3 @@ def _host_ask(master_dev, sigma, P):
     """NeuroEvolution.ask on the torch CPU generator (reference stream), uploaded."""
     m = master_dev.cpu()
     return torch.stack([m + torch.randn_like(m) * sigma for _ in range(P)]).to(master_dev.device)
-
-
-def _gather(gbuf, tr_f, tr_t, va_f, va_t, P, world, group):
-    n_max = gbuf.shape[2]
-    n = tr_f.shape[0]
-    mine = torch.zeros((4, n_max), dtype=torch.float64, device=tr_f.device)
-    mine[0, :n] = tr_f
-    mine[1, :n] = tr_t.to(torch.float64)
-    if va_f is not None:
-        mine[2, :n] = va_f
-        mine[3, :n] = va_t.to(torch.float64)
-    torch.distributed.all_gather_into_tensor(gbuf, mine, group=group)
-    counts = [shard_bounds(P, r, world)[1] - shard_bounds(P, r, world)[0] for r in range(world)]
-    parts = [gbuf[r, :, :counts[r]] for r in range(world)]
-    full = torch.cat(parts, dim=1)
-    out_va_f = full[2].contiguous() if va_f is not None else None
-    out_va_t = full[3].to(torch.int32) if va_f is not None else None
-    return full[0].contiguous(), full[1].to(torch.int32), out_va_f, out_va_t

@@ -1,0 +1,117 @@
+"""Population shards over ranks and the one exchange per generation.
+
+The reference evaluates the whole population in one process
+(Env/drl_engine.py:104-115, Pool.starmap).  Here rank r of a world of W owns
+the contiguous shard [r*n, min(P, (r+1)*n)) with n = ceil(P / W), regenerates
+its own genomes from the replicated master (counter-based, no genome traffic),
+rolls them out, and writes its results into a fixed-size per-rank record:
+
+    f64 fitness[2n]   train results at [0, n), validation results at [n, 2n)
+    i32 trades[2n]    same order
+    -> 24 n bytes
+
+One all-gather of the records (RCCL over xGMI; staged through host memory on
+the gloo backend) gives every rank the same [W, 24n]-byte array, which
+sgmm_ga_step reads in place: individual i's value is at byte offset
+(i // n) * 24n + field offset + (i % n) * element size.  Every rank then runs
+the identical step (argmax, master regeneration, sigma decay), so masters stay
+identical without a broadcast.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+def shard_capacity(P: int, world: int) -> int:
+    return -(-int(P) // int(world)) if P > 0 else 0
+
+
+def shard_bounds(P: int, rank: int, world: int):
+    """Contiguous population shard of a rank: [i0, i1) (may be empty)."""
+    n = shard_capacity(P, world)
+    i0 = min(P, rank * n)
+    return i0, min(P, i0 + n)
+
+
+# field byte offsets within a record of capacity n: (offset, element size)
+def field_layout(n: int):
+    return {"train_f": (0, 8), "val_f": (8 * n, 8), "train_t": (16 * n, 4), "val_t": (20 * n, 4)}
+
+
+def record_bytes(n: int) -> int:
+    return 24 * n
+
+
+def element_offset(i: int, n: int, field: str) -> int:
+    """Byte offset of individual i's `field` in the gathered records (the
+    addressing sgmm_ga_step implements with shard_n = n, shard_stride = 24n)."""
+    off, size = field_layout(n)[field]
+    return (i // n) * record_bytes(n) + off + (i % n) * size
+
+
+class FitnessRecords:
+    """The rank's record and the gathered records of all ranks."""
+
+    def __init__(self, P: int, world: int, device):
+        self.P, self.world = int(P), int(world)
+        n = self.n = shard_capacity(P, world)
+        self.device = torch.device(device)
+        self.rec = torch.zeros(record_bytes(n), dtype=torch.uint8, device=self.device)
+        f = self.rec[:16 * n].view(torch.float64)
+        t = self.rec[16 * n:].view(torch.int32)
+        self.f, self.t = f, t
+        self.train = (f[:n], t[:n])
+        self.val = (f[n:], t[n:])
+        self.both = (f, t)  # train then validation, for one fused launch of 2n episodes
+        self.gathered = torch.zeros(world * record_bytes(n), dtype=torch.uint8, device=self.device) \
+            if world > 1 else None
+        self._host = None
+
+    def all_gather(self, group=None):
+        """The generation's one collective.  RCCL gathers device buffers
+        directly; gloo (CPU tests, one-GPU rehearsals) goes through host memory."""
+        import torch.distributed as dist
+        if self.world == 1:
+            return
+        if self.device.type == "cuda" and dist.get_backend(group) == "gloo":
+            if self._host is None:
+                self._host = (torch.empty_like(self.rec, device="cpu"),
+                              torch.empty_like(self.gathered, device="cpu"))
+            src, dst = self._host
+            src.copy_(self.rec)
+            dist.all_gather_into_tensor(dst, src, group=group)
+            self.gathered.copy_(dst)
+        else:
+            dist.all_gather_into_tensor(self.gathered, self.rec, group=group)
+
+    def step_args(self):
+        """(fit, trades, val_fit, val_trades, P, shard_n, shard_stride): the
+        population arguments of sgmm_ga_step -- pointers into the gathered
+        records, or the local record read contiguously when world == 1."""
+        import ctypes
+        n = self.n
+        lay = field_layout(n)
+        base = (self.rec if self.world == 1 else self.gathered).data_ptr()
+        ptrs = tuple(ctypes.c_void_p(base + lay[k][0]) for k in ("train_f", "train_t", "val_f", "val_t"))
+        shard = (0, 0) if self.world == 1 else (n, record_bytes(n))
+        return ptrs + (self.P,) + shard
+
+    def population(self):
+        """Contiguous (train_f f64[P], train_t i32[P], val_f, val_t) of the whole
+        population (torch ops; for the separate tell/val-update entry points)."""
+        n, P = self.n, self.P
+        if self.world == 1:
+            return self.train[0][:P], self.train[1][:P], self.val[0][:P], self.val[1][:P]
+        g = self.gathered.view(self.world, record_bytes(n))
+        f = g[:, :16 * n].contiguous().view(torch.float64).view(self.world, 2 * n)
+        t = g[:, 16 * n:].contiguous().view(torch.int32).view(self.world, 2 * n)
+        return (f[:, :n].reshape(-1)[:P].contiguous(), t[:, :n].reshape(-1)[:P].contiguous(),
+                f[:, n:].reshape(-1)[:P].contiguous(), t[:, n:].reshape(-1)[:P].contiguous())
+
+
+def read_gathered(buf: np.ndarray, i: int, n: int, field: str):
+    """Host mirror of the kernel's shard addressing (tests)."""
+    off = element_offset(i, n, field)
+    dt = np.float64 if field.endswith("_f") else np.int32
+    return buf[off:off + np.dtype(dt).itemsize].view(dt)[0]

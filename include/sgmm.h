@@ -228,10 +228,16 @@ int sgmm_ga_val_update(sgmm_ga_state *state, const double *val_fitness,
  * NULL -- the ask() of the NEXT generation for individuals [i0, i0+n) with the
  * updated sigma (as sgmm_ga_ask; next_pop_adv likewise when master_adv).
  * Meant for modest P * n_params (one workgroup); use the separate entry points
- * for large populations. */
+ * for large populations.
+ * Sharded inputs (multi-GPU, after an all-gather of per-rank records): with
+ * shard_n > 0 the value of individual i in each of the four population arrays
+ * is read at byte offset (i / shard_n) * shard_stride + (i % shard_n) *
+ * sizeof(element) from its pointer; shard_n <= 0 means plain contiguous
+ * arrays.  Every rank runs the same step on the gathered records, so masters
+ * and sigma stay identical without a broadcast. */
 int sgmm_ga_step(sgmm_ga_state *state, const double *fitness, const int32_t *trades,
                  const double *val_fitness, const int32_t *val_trades, int32_t P,
-                 float *master_mm, float *master_adv, float *best_master,
+                 int32_t shard_n, int64_t shard_stride, float *master_mm, float *master_adv, float *best_master,
                  int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
                  sgmm_ga_history *history, int32_t history_cap,
                  float *next_pop_mm, float *next_pop_adv, int32_t i0, int32_t n, void *stream);

@@ -190,3 +190,78 @@ def test_device_ga_fitness_matches_reevaluation(sgmm, tmp_path):
     pol, hist = sess.finish()
     fv, _ = sgmm.evaluate_individual(pol.get_weights(), None, va, 0.0005, 0.001, 0.0, st)
     assert fv == max(hist["val_f"])
+
+
+@pytest.mark.parametrize("arl", [False, True])
+def test_ga_step_sharded_records_equal_contiguous(sgmm, arl):
+    """sgmm_ga_step reading gathered per-rank records (shard_n, shard_stride)
+    == reading contiguous population arrays."""
+    from sgmm_amd import _lib
+    from sgmm_amd.shard import FitnessRecords
+    G, P, W = 370, 10, 3
+    rng = np.random.default_rng(5)
+    f = rng.normal(size=P); f[7] = f.max() + 1.0
+    vf = rng.normal(size=P)
+    t = rng.integers(0, 900, P).astype(np.int32)
+    vt = rng.integers(0, 900, P).astype(np.int32)
+    recs = [FitnessRecords(P, W, DEV) for _ in range(W)]
+    gathered = torch.cat([r.rec for r in _fill(recs, f, t, vf, vt, P, W)])
+    runs = []
+    for sharded in (False, True):
+        L, st = _state(sgmm, sigma=0.1)
+        torch.manual_seed(1)
+        master = torch.randn(G, device=DEV)
+        madv = torch.randn(1250, device=DEV) if arl else None
+        best = torch.zeros(G, device=DEV)
+        hist = torch.zeros((2, 40), dtype=torch.uint8, device=DEV)
+        if sharded:
+            r = recs[0]
+            r.gathered = gathered
+            r.world = W
+            args = r.step_args()
+        else:
+            cols = [torch.tensor(x, device=DEV) for x in (f, t, vf, vt)]
+            args = tuple(_lib.ptr(c) for c in cols) + (P, 0, 0)
+        _lib.check(L.sgmm_ga_step(_lib.ptr(st), *args, _lib.ptr(master), _lib.ptr(madv) if arl else None,
+                                  _lib.ptr(best), G, 1250 if arl else 0, 9, _lib.ptr(hist), 2, None, None, 0, 0,
+                                  _lib.stream_ptr()), "ga_step")
+        torch.cuda.synchronize()
+        runs.append((st.cpu(), master.cpu(), None if madv is None else madv.cpu(), best.cpu(), hist.cpu()))
+    for a, b in zip(*runs):
+        assert (a is None and b is None) or torch.equal(a, b)
+    s = _read_state(runs[0][0])
+    assert s["best_idx"] == 7 and s["adv_best_idx"] == int(np.argmax(-f))
+
+
+def _fill(recs, f, t, vf, vt, P, W):
+    from sgmm_amd.shard import shard_bounds
+    for r, rec in enumerate(recs):
+        i0, i1 = shard_bounds(P, r, W)
+        n = i1 - i0
+        rec.train[0][:n] = torch.tensor(f[i0:i1], device=DEV)
+        rec.train[1][:n] = torch.tensor(t[i0:i1], device=DEV)
+        rec.val[0][:n] = torch.tensor(vf[i0:i1], device=DEV)
+        rec.val[1][:n] = torch.tensor(vt[i0:i1], device=DEV)
+    return recs
+
+
+def test_drlengine_two_ranks_equal_one(sgmm, tmp_path):
+    """DRLEngine over 2 ranks (gloo exchange, both ranks on this GPU; the HIP
+    graphs split around the all-gather) reproduces the single-process run."""
+    import socket
+    import torch.multiprocessing as mp
+    import _shard_ranks as R
+    P, gens = 24, 9
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    mp.spawn(R.train_rank, args=(2, port, P, gens, str(tmp_path)), nprocs=2, join=True)
+    sg, tr, va, st, _ = R.workload(P, T=400, Tv=150)
+    torch.manual_seed(0)
+    eng = sg.DRLEngine(pop_size=P, phi=0.0005, tick_size=0.001, save_dir=str(tmp_path / "single"), hidden_dim=16,
+                       rng="device", seed=11, verbose=False, sync_every=4, patience=3, dist=False)
+    pol, hist = eng.train(tr, va, st, generations=gens)
+    for r in range(2):
+        o = np.load(tmp_path / f"t{r}.npz")
+        for k in hist:
+            assert np.array_equal(o[k], np.array(hist[k], np.float64)), (r, k)
+        assert np.array_equal(o["w"], pol.get_weights().numpy())
+        assert float(o["sigma"]) == eng.mm_evolver.sigma
