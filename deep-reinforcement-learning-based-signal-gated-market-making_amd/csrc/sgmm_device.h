@@ -30,11 +30,11 @@ __device__ __forceinline__ float relu(float a) {
 
 // float -> int action: saturating, NaN -> INT32_MIN (the x86 cvtt value numpy's
 // astype(int) produces).  Values are already integral (rint) when called.
+// Branch-free: fmaxf maps NaN to the lower clamp, so NaN and -inf both land
+// on -2^31; the upper clamp is the largest float below 2^31.
 __device__ __forceinline__ int32_t act_to_int(float r) {
-    if (r != r) return INT32_MIN;
-    if (r >= 2147483520.0f) return INT32_MAX;
-    if (r <= -2147483648.0f) return INT32_MIN;
-    return (int32_t)r;
+    const int32_t v = (int32_t)fminf(fmaxf(r, -2147483648.0f), 2147483520.0f);
+    return r >= 2147483520.0f ? INT32_MAX : v;
 }
 
 // ---------------------------------------------------------------- FTPEnv.step
@@ -56,24 +56,16 @@ __device__ __forceinline__ StepOut ftp_step(const sgmm_env_params& p, int32_t in
     const double qb = best_bid - (double)off_b * p.tick;   // market_env.py:31
     o.fill_buy = (inv < p.i_max) && (qb >= sell_min);      // :34,:37 (NaN -> no fill)
     o.fill_sell = (inv > p.i_min) && (qa <= buy_max);      // :35,:38
-    double pnl = 0.0, fees = 0.0;
-    int32_t q = inv;
-    o.cash_delta_buy = 0.0;
-    o.cash_delta_sell = 0.0;
-    if (o.fill_buy) {                                      // :44-49
-        const double f = qb * p.fee;
-        q += 1;
-        o.cash_delta_buy = qb + f;
-        pnl += (mid_next - qb) - f;
-        fees += f;
-    }
-    if (o.fill_sell) {                                     // :50-55
-        const double f = qa * p.fee;
-        q -= 1;
-        o.cash_delta_sell = qa - f;
-        pnl += (qa - mid_next) - f;
-        fees += f;
-    }
+    // both sides computed, then selected: the same operations in the same
+    // order as the reference's conditional updates (no branches on the GPU)
+    const double fb = qb * p.fee, fs = qa * p.fee;         // :44-55
+    const double pnl_b = o.fill_buy ? 0.0 + ((mid_next - qb) - fb) : 0.0;
+    const double pnl = o.fill_sell ? pnl_b + ((qa - mid_next) - fs) : pnl_b;
+    const double fee_b = o.fill_buy ? 0.0 + fb : 0.0;
+    const double fees = o.fill_sell ? fee_b + fs : fee_b;
+    o.cash_delta_buy = o.fill_buy ? qb + fb : 0.0;
+    o.cash_delta_sell = o.fill_sell ? qa - fs : 0.0;
+    const int32_t q = inv + o.fill_buy - o.fill_sell;
     o.inv = q;
     o.pnl = pnl;
     o.fee_paid = fees;

@@ -11,8 +11,8 @@
 //     but the policy only sees (signal_t, inventory) and the inventory takes
 //     at most 8 values (caps +-2 -> 5).  So the policy, the FPT fill test and
 //     the reward are evaluated for EVERY (tick, inventory[, adversary flags])
-//     state in parallel.  H >= 16: k_policy_table_mfma, the two H-wide layers
-//     on v_mfma_f32_16x16x4_f32 (whose k-ordered fused chain IS the canonical
+//     state in parallel.  H >= 16: k_policy_table_mfma, the H x H layer on
+//     v_mfma_f32_16x16x4_f32 (whose k-ordered fused chain IS the canonical
 //     dot-product order); H = 8 or SGMM_TABLE_PATH=valu: k_policy_table, one
 //     lane per (tick, state) on the VALU.  Output per tick: the exclusive
 //     prefix transition map of its 64-tick chunk (+ traded mask) and one
@@ -194,25 +194,62 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + blockIdx.x] = inc;
 }
 
+#ifdef SGMM_STAMPS
+// diagnostic build only: phase timestamps (s_memtime) of the scan kernel per
+// episode and of the table kernel per wave; slot 7 of a table wave holds
+// s_memrealtime at entry (a clock common to all XCDs)
+__device__ unsigned long long g_stamps[4096][8];
+__device__ unsigned long long g_tstamps[8192][8];
+#define SGMM_STAMP(e, k)                                                           \
+    do {                                                                           \
+        unsigned long long t_;                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        if (threadIdx.x == 0 && (e) < 4096) g_stamps[e][k] = t_;                   \
+    } while (0)
+#define SGMM_TSTAMP(w, k, dep)                                                     \
+    do {                                                                           \
+        unsigned long long t_;                                                     \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" \
+                     : "=s"(t_) : "v"(dep) : "memory");                             \
+        if ((threadIdx.x & 63) == 0 && (w) < 8192) g_tstamps[w][k] = t_;           \
+    } while (0)
+#define SGMM_TSTAMP_REAL(w, k)                                                         \
+    do {                                                                               \
+        unsigned long long t_;                                                         \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        if ((threadIdx.x & 63) == 0 && (w) < 8192) g_tstamps[w][k] = t_;               \
+    } while (0)
+#else
+#define SGMM_STAMP(e, k) \
+    do {                 \
+    } while (0)
+#define SGMM_TSTAMP(w, k, dep) \
+    do {                       \
+    } while (0)
+#define SGMM_TSTAMP_REAL(w, k) \
+    do {                       \
+    } while (0)
+#endif
+
 // ------------------------------------------------------------------ table on the matrix cores
 // gfx950's f32-input MFMA v_mfma_f32_16x16x4_f32 computes, per output, the
 // k-ordered fused chain D = fma(a_k3,b_k3, fma(.., fma(a_k0,b_k0, C))) --
 // exactly the canonical dot-product order of the numerics contract -- so the
-// policy's two H-wide layers run on the matrix pipe bit-identically to the
+// policy's H x H layer runs on the matrix pipe bit-identically to the
 // VALU/oracle chains, with the weights held as compact per-lane fragments
-// (loaded once per wave, reused for every tile) instead of being streamed
-// through scalar loads.
+// (loaded once per wave, reused for every tile).
 //
-// One wave = one 64-tick chunk of one episode, all inventory states:
-// 16-sample tiles (state si, ticks 16q..16q+15 of the chunk).
-//   layer 2:  H2^T[j][n] = W2[j][:] . H1^T[:][n] + b2[j]   (A = W2 rows, B = h1 of
-//             sample n at k = 4i + (lane>>4); C = b2 broadcast)
-//   layer 3:  OUT[o][n] = W3[o][:] . relu(H2^T)[:][n] + b3[o]  (rows o = 0,1 of a
-//             16-row tile; B = the layer-2 accumulator registers as they stand)
-// Rows of W2 are permuted so that row 4g+r of row-tile rt is neuron
-// 16rt + 4r + g: the layer-3 MFMA k-step s = 4rt + r then reads, in lane group
-// g, neuron 4s + g from its own register r of tile rt, i.e. neurons
-// 0,1,2,...,H-1 in order -- the canonical layer-3 chain, with no lane movement.
+// One wave = one 64-tick chunk of one episode; for each inventory state:
+//   layer 1 (VALU):  h1[k][n] = relu(b1 + W1[k].(s1n, s2n, inv/2)), the two
+//                    signal terms shared by all states;
+//   layer 2 (MFMA):  H2^T[j][n] = W2[j][:] . H1^T[:][n] + b2[j], four 16-sample
+//                    tiles (A = W2 rows, B = h1 at k = 4i + (lane>>4), C = b2);
+//   transpose:       relu(H2) -> LDS as [sample][neuron] (one 16-byte write
+//                    per tile and lane);
+//   layer 3 (VALU):  lane n = tick n reads its H activations and runs the two
+//                    canonical output chains b3[o] + sum_j W3[o][j] h2[j] (the
+//                    2-row output would waste 7/8 of a 16-row MFMA tile).
+// The lane then holds the policy outputs of its own tick for every state.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 template <int H, int NSI, bool ARL>
@@ -223,8 +260,9 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     static_assert(H % 16 == 0, "MFMA table needs H multiple of 16");
     using L = GenomeLayout<H>;
-    constexpr int NT = H / 16;  // 16-neuron row tiles of layer 2
-    constexpr int KS = H / 4;   // k-steps (4 per MFMA)
+    constexpr int NT = H / 16;   // 16-neuron row tiles of layer 2
+    constexpr int KS = H / 4;    // k-steps (4 per MFMA)
+    constexpr int HP = H + 4;    // LDS row pitch (floats) of the transposed activations
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
     const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -232,99 +270,105 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     if (t0 >= T) return;  // wave-uniform; no block barriers below
     const int lane = threadIdx.x & (kWave - 1), grp = lane >> 4, col = lane & 15;
     const int ns = ARL ? 4 * nsi : nsi;
+#ifdef SGMM_STAMPS
+    const int wslot = e * (int)(gridDim.x * 4) + chunk;
+#endif
+    SGMM_TSTAMP_REAL(wslot, 7);
+    SGMM_TSTAMP(wslot, 0, 0);
     const sgmm_env_params p = params[ep.param[e]];
     const float* __restrict__ g = mm + (int64_t)ep.genome[e] * mm_stride;
+    const int64_t row = ep.step_off[e] + t0 + lane;  // this lane's output row
+    __shared__ __attribute__((aligned(16))) float hb_s[4][kWave * HP];
+    float* hb = hb_s[threadIdx.x >> 6];
 
     // ---- per-lane weight fragments (lane-dependent, tile-independent)
-    float w2f[NT][KS];  // A of layer 2: row col of tile rt, k = 4i + grp
-    f32x4 b2c[NT];      // C of layer 2: row 4grp + r of tile rt
+    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
+    f32x4 b2c[NT];      // C of layer 2: neurons 16rt + 4grp + r
 #pragma unroll
     for (int rt = 0; rt < NT; ++rt) {
-        const int jrow = 16 * rt + 4 * (col & 3) + (col >> 2);  // permuted neuron of row col
 #pragma unroll
-        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + jrow * H + 4 * i + grp];
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + (16 * rt + col) * H + 4 * i + grp];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * r + grp];
+        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * grp + r];
     }
-    float w1f[KS][4];   // layer 1 for k = 4i + grp: W1[k][0..2], b1[k]
+    float w1s[KS];      // layer-1 inventory weight W1[k][2] for k = 4i + grp
+    float pre[4][KS];   // b1[k] + W1[k][0] s1n + W1[k][1] s2n of sample 16q + col
+    {
+        float xs0[4], xs1[4];
 #pragma unroll
-    for (int i = 0; i < KS; ++i) {
-        const int k = 4 * i + grp;
-        w1f[i][0] = g[L::W1 + 3 * k];
-        w1f[i][1] = g[L::W1 + 3 * k + 1];
-        w1f[i][2] = g[L::W1 + 3 * k + 2];
-        w1f[i][3] = g[L::B1 + k];
-    }
-    float w3f[KS];      // A of layer 3: row col (= output o), k-step s -> neuron 4s + grp
-#pragma unroll
-    for (int s2 = 0; s2 < KS; ++s2) w3f[s2] = col < 2 ? g[L::W3 + col * H + 4 * s2 + grp] : 0.0f;
-    f32x4 b3c;          // C of layer 3: row 4grp + r = output o
-#pragma unroll
-    for (int r = 0; r < 4; ++r) b3c[r] = (grp == 0 && r < 2) ? g[L::B3 + r] : 0.0f;
-
-    // ---- the policy for every (state, tick) of the chunk.  The NSI states of a
-    // 16-tick group are independent MFMA chains: issuing them interleaved
-    // (k-step outer, state inner) keeps the matrix pipe fed despite the
-    // dependent-accumulator latency of each chain.
-    float out0[NSI], out1[NSI];
-#pragma unroll
-    for (int si = 0; si < NSI; ++si) out0[si] = out1[si] = 0.0f;
-    float x2[NSI];
-#pragma unroll
-    for (int si = 0; si < NSI; ++si) x2[si] = (float)((double)(inv_min + si) / 2.0);
-    float xs0[4], xs1[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int tq = min(t0 + 16 * q + col, T - 1);  // clamp: padded samples are discarded
-        const int64_t ti = ep.tick_off[e] + tq;
-        xs0[q] = tk.s1n[ti];
-        xs1[q] = tk.s2n[ti];
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        float pre[KS];
-#pragma unroll
-        for (int i = 0; i < KS; ++i)
-            pre[i] = __builtin_fmaf(w1f[i][1], xs1[q], __builtin_fmaf(w1f[i][0], xs0[q], w1f[i][3]));
-        f32x4 acc[NSI][NT];
-#pragma unroll
-        for (int si = 0; si < NSI; ++si)
-#pragma unroll
-            for (int rt = 0; rt < NT; ++rt) acc[si][rt] = b2c[rt];
+        for (int q = 0; q < 4; ++q) {
+            const int tq = min(t0 + 16 * q + col, T - 1);  // clamp: padded samples are discarded
+            const int64_t ti = ep.tick_off[e] + tq;
+            xs0[q] = tk.s1n[ti];
+            xs1[q] = tk.s2n[ti];
+        }
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
+            const int k = 4 * i + grp;
+            const float a0 = g[L::W1 + 3 * k], a1 = g[L::W1 + 3 * k + 1], bb = g[L::B1 + k];
+            w1s[i] = g[L::W1 + 3 * k + 2];
 #pragma unroll
-            for (int si = 0; si < NSI; ++si) {
-                const float h1 = relu(__builtin_fmaf(w1f[i][2], x2[si], pre[i]));
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt)
-                    acc[si][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, acc[si][rt], 0, 0, 0);
-            }
-        }
-        f32x4 o[NSI];
-#pragma unroll
-        for (int si = 0; si < NSI; ++si) o[si] = b3c;
-#pragma unroll
-        for (int s2 = 0; s2 < KS; ++s2)
-#pragma unroll
-            for (int si = 0; si < NSI; ++si)
-                o[si] = __builtin_amdgcn_mfma_f32_16x16x4f32(w3f[s2], relu(acc[si][s2 >> 2][s2 & 3]),
-                                                             o[si], 0, 0, 0);
-        // rows 0/1 of group 0 hold the outputs of sample col: give tick 16q + c
-        // (lane 16q + c) its pair
-#pragma unroll
-        for (int si = 0; si < NSI; ++si) {
-            const float v0 = __shfl(o[si][0], col, kWave), v1 = __shfl(o[si][1], col, kWave);
-            if (grp == q) {
-                out0[si] = v0;
-                out1[si] = v1;
-            }
+            for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(a1, xs1[q], __builtin_fmaf(a0, xs0[q], bb));
         }
     }
+    // this lane's tick record for the FPT step, fetched now so its latency
+    // hides under the policy evaluation
+    const int64_t tix = ep.tick_off[e] + min(t0 + lane, T - 1);
+    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
+    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
+    SGMM_TSTAMP(wslot, 1, w2f[0][0] + w1s[KS - 1] + pre[3][KS - 1] + b2c[0][0]);
+
+    // ---- the policy for every (state, tick) of the chunk
+    float out0[NSI], out1[NSI];
+#pragma unroll
+    for (int si = 0; si < NSI; ++si) {
+        out0[si] = out1[si] = 0.0f;
+        if (si >= nsi) continue;
+        const float x2 = (float)((double)(inv_min + si) / 2.0);
+        f32x4 acc[4][NT];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) acc[q][rt] = b2c[rt];
+        // four independent 16-sample chains, issued interleaved (k-step outer)
+#pragma unroll
+        for (int i = 0; i < KS; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt)
+                    acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, acc[q][rt], 0, 0, 0);
+            }
+        // transpose relu(H2) through LDS: lane n gets tick n's H activations
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+                *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+            }
+        __builtin_amdgcn_wave_barrier();
+        float o0 = g[L::B3], o1 = g[L::B3 + 1];
+#pragma unroll
+        for (int j4 = 0; j4 < H / 4; ++j4) {
+            const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                o0 = __builtin_fmaf(g[L::W3 + 4 * j4 + r], h[r], o0);
+                o1 = __builtin_fmaf(g[L::W3 + H + 4 * j4 + r], h[r], o1);
+            }
+        }
+        out0[si] = o0;
+        out1[si] = o1;
+        __builtin_amdgcn_wave_barrier();
+    }
+    SGMM_TSTAMP(wslot, 2, out0[NSI - 1] + out1[0]);
 
     // ---- FPT step from every state, one lane per tick
     const bool valid = t0 + lane < T;
-    const int64_t row = ep.step_off[e] + t0 + lane;
     __shared__ int32_t lut_s[4][2][32];
     int32_t* lut0 = lut_s[threadIdx.x >> 6][0];
     int32_t* lut1 = lut_s[threadIdx.x >> 6][1];
@@ -344,9 +388,7 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     uint32_t map = kIdentityMap, traded = 0;
     uint64_t fw = 0;
     if (valid) {
-        const int64_t ti = ep.tick_off[e] + t0 + lane;
-        const double mid = tk.mid_next[ti], ask = tk.best_ask[ti], bid = tk.best_bid[ti];
-        const double bmax = tk.buy_max[ti], smin = tk.sell_min[ti];
+        const double mid = tmid, ask = task, bid = tbid, bmax = tbmax, smin = tsmin;
         double* __restrict__ R = rew + row * ns;
         map = 0;
 #pragma unroll
@@ -376,6 +418,7 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
         if (valid) fills[row] = fw;
         return;
     }
+    SGMM_TSTAMP(wslot, 3, map + traded);
     uint32_t inc = map;
 #pragma unroll
     for (int d = 1; d < kWave; d <<= 1) {
@@ -384,8 +427,13 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     }
     uint32_t excl = __shfl_up(inc, 1, kWave);
     if (lane == 0) excl = kIdentityMap;
+    SGMM_TSTAMP(wslot, 4, excl);
     if (valid) words[row] = (excl & 0x00FFFFFFu) | (traded << 24);
     if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + chunk] = inc;
+#ifdef SGMM_STAMPS
+    SGMM_TSTAMP(wslot, 5, 0);
+    SGMM_TSTAMP_REAL(wslot, 6);
+#endif
 }
 
 // ------------------------------------------------------------------ path scan (no adversary)
@@ -402,20 +450,6 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
 // workgroup barrier between windows.
 constexpr int kScanThreads = 1024;
 
-#ifdef SGMM_STAMPS
-// diagnostic build only: per-episode phase timestamps of the scan kernel
-__device__ unsigned long long g_stamps[4096][8];
-#define SGMM_STAMP(e, k)                                                           \
-    do {                                                                           \
-        unsigned long long t_;                                                     \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-        if (threadIdx.x == 0 && (e) < 4096) g_stamps[e][k] = t_;                   \
-    } while (0)
-#else
-#define SGMM_STAMP(e, k) \
-    do {                 \
-    } while (0)
-#endif
 constexpr int kScanWin = 4096;         // ticks resident per window (32 KB of rewards)
 constexpr int kReadySeg = 256;         // ticks per ready counter
 
@@ -850,6 +884,9 @@ using namespace sgmm;
 #ifdef SGMM_STAMPS
 extern "C" int sgmm_debug_stamps(unsigned long long* host, int n_eps) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n_eps);
+}
+extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * n_waves);
 }
 #endif
 
