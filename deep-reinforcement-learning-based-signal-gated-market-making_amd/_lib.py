@@ -90,6 +90,7 @@ SIGNATURES = {
     "sgmm_ga_val_update": (ctypes.c_int, [_VP, _VP, _VP, _I32, _VP, _VP, _I64, _VP, _I32, _VP]),
     "sgmm_ga_step": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP, _VP, _I64, _I64, _U64,
                                     _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
+    "sgmm_ordered_sum": (ctypes.c_int, [_VP, _I64, ctypes.c_double, _VP, _VP]),
     "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "sgmm_profile_read": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
 }

@@ -154,6 +154,74 @@ __device__ __forceinline__ void adv_delta(const float* __restrict__ g, const sgm
     db = act_to_int(rintf(r1 * p.adv_scale));
 }
 
+// ---------------------------------------------------------------- cross-lane (DPP)
+// Data-parallel-primitive moves: a VALU operand modifier, no LDS round trip.
+// Lanes whose source is outside the row (or whose row is masked off) get
+// `old`.  GFX9 controls: row_shr:n = 0x110 + n, row_bcast:15 = 0x142,
+// row_bcast:31 = 0x143.
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
+    const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)old, (uint32_t)v);
+    const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(old >> 32), (uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ double dppf64(double old, double v) {
+    return __longlong_as_double((long long)dpp64<CTRL, ROW_MASK>((uint64_t)__double_as_longlong(old),
+                                                                 (uint64_t)__double_as_longlong(v)));
+}
+// inclusive prefix sums within rows of 16 lanes / over the wave
+__device__ __forceinline__ uint64_t row_scan_add(uint64_t v) {
+    v += dpp64<0x111>(0, v);
+    v += dpp64<0x112>(0, v);
+    v += dpp64<0x114>(0, v);
+    v += dpp64<0x118>(0, v);
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_scan_add(uint64_t v) {
+    v = row_scan_add(v);
+    v += dpp64<0x142, 0xA>(0, v);
+    v += dpp64<0x143, 0xC>(0, v);
+    return v;
+}
+__device__ __forceinline__ double row_scan_addf(double v) {
+    v += dppf64<0x111>(0.0, v);
+    v += dppf64<0x112>(0.0, v);
+    v += dppf64<0x114>(0.0, v);
+    v += dppf64<0x118>(0.0, v);
+    return v;
+}
+__device__ __forceinline__ double wave_scan_addf(double v) {
+    v = row_scan_addf(v);
+    v += dppf64<0x142, 0xA>(0.0, v);
+    v += dppf64<0x143, 0xC>(0.0, v);
+    return v;
+}
+// inclusive min / max scans within rows of 16 lanes (signed 64-bit)
+__device__ __forceinline__ int64_t row_scan_min(int64_t v) {
+    v = min(v, (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)v));
+    v = min(v, (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)v));
+    v = min(v, (int64_t)dpp64<0x114>((uint64_t)INT64_MAX, (uint64_t)v));
+    v = min(v, (int64_t)dpp64<0x118>((uint64_t)INT64_MAX, (uint64_t)v));
+    return v;
+}
+__device__ __forceinline__ int64_t row_scan_max(int64_t v) {
+    v = max(v, (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)v));
+    v = max(v, (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)v));
+    v = max(v, (int64_t)dpp64<0x114>((uint64_t)INT64_MIN, (uint64_t)v));
+    v = max(v, (int64_t)dpp64<0x118>((uint64_t)INT64_MIN, (uint64_t)v));
+    return v;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // ---------------------------------------------------------------- Philox4x32-10
 struct U4 { uint32_t x, y, z, w; };
 

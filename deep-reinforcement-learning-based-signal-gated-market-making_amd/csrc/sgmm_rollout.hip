@@ -198,7 +198,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
 // diagnostic build only: phase timestamps (s_memtime) of the scan kernel per
 // episode and of the table kernel per wave; slot 7 of a table wave holds
 // s_memrealtime at entry (a clock common to all XCDs)
-__device__ unsigned long long g_stamps[4096][8];
+__device__ unsigned long long g_stamps[4096][16];
 __device__ unsigned long long g_tstamps[8192][8];
 #define SGMM_STAMP(e, k)                                                           \
     do {                                                                           \
@@ -436,22 +436,230 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
 #endif
 }
 
+// ------------------------------------------------------------------ exact ordered sum
+// The episode total is the reference's sequential float64 sum
+// (drl_engine.py:53: total = ((0 + r0) + r1) + ...).  It is evaluated in
+// parallel, bit-exactly, from one property of IEEE addition: while the running
+// sum S stays inside one binade [2^e, 2^(e+1)) (either sign) it is an integer
+// multiple M of u = 2^(e-52), and fl(S + r) = (M + rint(r/u)) * u exactly as
+// long as the exact S + r stays inside the binade and r/u is not a tie (x.5).
+// So a stretch of ticks that keeps one binade adds up as 64-bit integers.
+//   1. blocks of 16 ticks: approximate sums (any order) -> approximate start
+//      of every block -> predicted binade of every block;
+//   2. per block and predicted binade: integer steps d = rint(r/u), their
+//      16-lane prefix (end, min, max) and a flag for ties / huge steps;
+//   3. one wave walks the blocks from the exact S: a run of blocks whose
+//      predicted binade is S's and whose prefix range keeps M strictly inside
+//      [2^52, 2^53) is added in one integer prefix; the first block that fails
+//      (binade change, tie, zero/subnormal S, NaN) is added sequentially in
+//      float64 -- the reference operation -- and the walk resumes after it.
+// Every accepted shortcut is exact by the property above, so the result is
+// the sequential sum bit for bit.
+constexpr int kSumBlk = 16;
+constexpr int kScanThreads = 1024;
+constexpr int kScanWin = 4096;  // ticks resident per window (32 KB of rewards)
+constexpr int kScanBlks = kScanWin / kSumBlk;
+constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
+
+// S = M * 2^(e-52) with |M| in [2^52, 2^53); false unless S is normal with
+// |e| <= 900 (the shortcut's range: 2^(52-e) and its inverse stay normal)
+__device__ __forceinline__ bool binade_of(double s, int& e, int64_t& m) {
+    const int64_t bits = __double_as_longlong(s);
+    const int be = (int)((bits >> 52) & 0x7FF);
+    e = be - 1023;
+    const int64_t mag = (bits & 0xFFFFFFFFFFFFFLL) | (1LL << 52);
+    m = bits < 0 ? -mag : mag;
+    return be >= 1023 - 900 && be <= 1023 + 900;
+}
+
+__device__ __forceinline__ double from_binade(int64_t m, int e) {
+    const int64_t mag = m < 0 ? -m : m;  // in [2^52, 2^53)
+    const int64_t bits = ((int64_t)(e + 1023) << 52) | (mag - (1LL << 52));
+    return __longlong_as_double(m < 0 ? (bits | INT64_MIN) : bits);
+}
+
+__device__ __forceinline__ double uniform_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ double pow2(int k) {  // k in [-1022, 1023]
+    return __longlong_as_double((int64_t)(k + 1023) << 52);
+}
+
+struct SumScratch {
+    double* approx;   // [nblk] approximate block sums, then block starts
+    int32_t* be;      // [nblk] predicted binade (INT32_MIN: none)
+    int64_t* pend;    // [nblk] integer step sum of the block
+    int64_t* pmin;    // [nblk] min / max of its inclusive prefixes
+    int64_t* pmax;
+    uint64_t* z;      // [nblk] exclusive prefix of pend (mod 2^64; meaningful across same-binade runs)
+    uint8_t* bad;     // [nblk] tie / huge step / no binade
+};
+
+// All NT threads call; returns the exact sequential sum S + sel[0] + ... +
+// sel[n-1] in wave 0 (other waves: unspecified).  Ends with a barrier.
+template <int NT>
+__device__ double exact_ordered_sum(const double* sel, int n, double S, SumScratch sc) {
+    static_assert(NT % kWave == 0, "whole waves");
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), k = tid & (kSumBlk - 1);
+    const int nblk = (n + kSumBlk - 1) / kSumBlk;
+    const int span = nblk * kSumBlk;
+    // 1a. approximate block sums (any order)
+    constexpr int kIt = (kScanWin + NT - 1) / NT;  // strided passes per thread
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int i = tid + it * NT;
+        if (i < span) {  // uniform per 16-lane row
+            const double v = row_scan_addf(i < n ? sel[i] : 0.0);
+            if (k == kSumBlk - 1) sc.approx[i / kSumBlk] = v;
+        }
+    }
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 8);
+    // 1b. approximate block starts (wave 0)
+    if (tid < kWave) {
+        double carry = S;
+        for (int b0 = 0; b0 < nblk; b0 += kWave) {
+            const int b = b0 + lane;
+            const double v = b < nblk ? sc.approx[b] : 0.0;
+            const double inc = wave_scan_addf(v);
+            if (b < nblk) sc.approx[b] = carry + (inc - v);
+            carry += __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(inc), kWave - 1));
+        }
+    }
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 9);
+    // 2. integer steps per block in its predicted binade
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+        const int i = tid + it * NT;
+        if (i >= span) continue;  // uniform per 16-lane row
+        const int b = i / kSumBlk;
+        int e;
+        int64_t mdummy;
+        const bool fast = binade_of(sc.approx[b], e, mdummy);
+        int64_t d = 0;
+        bool bad = !fast;
+        if (fast && i < n) {
+            const double q = sel[i] * pow2(52 - e);
+            bad = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
+            d = bad ? 0 : (int64_t)rint(q);
+        }
+        const int64_t P = (int64_t)row_scan_add((uint64_t)d);
+        const int64_t mn = row_scan_min(P), mx = row_scan_max(P);
+        const uint64_t bl = __ballot(bad);
+        if (k == kSumBlk - 1) {
+            sc.be[b] = fast ? e : INT32_MIN;
+            sc.pend[b] = P;
+            sc.pmin[b] = mn;
+            sc.pmax[b] = mx;
+            sc.bad[b] = ((bl >> (lane & ~(kSumBlk - 1))) & 0xFFFFu) != 0;
+        }
+    }
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 10);
+    // 3. the walk (wave 0; every lane carries the same S)
+    if (tid < kWave) {
+        uint64_t zcarry = 0;  // exclusive prefix of the block sums, wrapping
+        for (int b0 = 0; b0 < nblk; b0 += kWave) {
+            const int b = b0 + lane;
+            const uint64_t v = b < nblk ? (uint64_t)sc.pend[b] : 0;
+            const uint64_t inc = wave_scan_add(v);
+            if (b < nblk) sc.z[b] = zcarry + (inc - v);
+            zcarry += readlane64(inc, kWave - 1);
+        }
+        SGMM_STAMP(blockIdx.x, 11);
+#ifdef SGMM_STAMPS
+        unsigned long long n_iter = 0, n_slow = 0, slow_cyc = 0, fast_cyc = 0;
+#endif
+        for (int g0 = 0; g0 < nblk; g0 += kWave) {
+            const int lim = min(kWave, nblk - g0);
+            const int b = g0 + lane;
+            const bool inb = lane < lim;
+            const int eb = inb ? sc.be[b] : INT32_MIN;
+            const int64_t pe = inb ? sc.pend[b] : 0, pmn = inb ? sc.pmin[b] : 0, pmx = inb ? sc.pmax[b] : 0;
+            const uint64_t zb = inb ? sc.z[b] : 0;
+            const bool bd = inb ? sc.bad[b] != 0 : true;
+            const uint64_t live = lim == kWave ? ~0ull : ((1ull << lim) - 1);
+            int pos = 0;
+            while (pos < lim) {
+#ifdef SGMM_STAMPS
+                ++n_iter;
+                unsigned long long tf0_;
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tf0_) : "v"(S) : "memory");
+#endif
+                S = uniform_f64(S);  // wave-uniform: scalar control flow below
+                int f = pos, e;
+                int64_t M;
+                if (binade_of(S, e, M)) {
+                    // M at the start of this lane's block if blocks pos.. are all accepted
+                    const int64_t c = M + (int64_t)(zb - readlane64(zb, pos));
+                    const bool okp = c + pmn >= kMLo && c + pmx <= kMHi;
+                    const bool okn = c + pmx <= -kMLo && c + pmn >= -kMHi;
+                    const bool ok = lane < pos || (inb && eb == e && !bd && (M > 0 ? okp : okn));
+                    const uint64_t fails = __ballot(!ok) & live;
+                    f = fails ? __ffsll((unsigned long long)fails) - 1 : lim;
+                    if (f > pos) {
+                        const uint64_t ce = (uint64_t)(f < lim ? c : c + pe);
+                        S = from_binade((int64_t)readlane64(ce, f < lim ? f : lim - 1), e);
+                    }
+                }
+#ifdef SGMM_STAMPS
+                {
+                    unsigned long long tf1_;
+                    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tf1_) : "v"(S), "s"(f) : "memory");
+                    fast_cyc += tf1_ - tf0_;
+                }
+#endif
+                if (f < lim) {  // this block the reference way
+#ifdef SGMM_STAMPS
+                    ++n_slow;
+                    unsigned long long ts0_;
+                    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts0_)::"memory");
+#endif
+                    const int t0 = (g0 + f) * kSumBlk, m = min(kSumBlk, n - t0);
+                    double v[kSumBlk];  // all loads in flight before the dependent adds
+#pragma unroll
+                    for (int j = 0; j < kSumBlk; ++j) v[j] = sel[t0 + min(j, m - 1)];
+                    if (m == kSumBlk) {
+#pragma unroll
+                        for (int j = 0; j < kSumBlk; ++j) S += v[j];
+                    } else {
+                        for (int j = 0; j < m; ++j) S += v[j];
+                    }
+#ifdef SGMM_STAMPS
+                    {
+                        unsigned long long ts1_;
+                        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts1_) : "v"(S) : "memory");
+                        slow_cyc += ts1_ - ts0_;
+                    }
+#endif
+                    pos = f + 1;
+                } else {
+                    pos = lim;
+                }
+            }
+        }
+        SGMM_STAMP(blockIdx.x, 12);
+#ifdef SGMM_STAMPS
+        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; g_stamps[blockIdx.x][15] = slow_cyc; g_stamps[blockIdx.x][7] = fast_cyc; }
+#endif
+    }
+    __syncthreads();
+    return S;
+}
+
 // ------------------------------------------------------------------ path scan (no adversary)
 // One workgroup (16 waves) per episode.
-//   1. all waves: the episode's prefix words -> LDS (one coalesced pass);
-//      wave 0: chunk start states from a wave-level scan of the chunk maps;
-//   2. waves 1..15 (producers): per tick, state = one field of its prefix word,
-//      gather the reward of that state into LDS sel[t], count trades, and
-//      publish each finished 256-tick segment with an LDS counter;
-//   3. thread 0 (consumer): adds sel[] in tick order as segments become
-//      ready (drl_engine.py:54: total = ((r0 + r1) + r2) + ..., float64) --
-//      the only serial part of the rollout, fed from LDS three loads ahead.
-// Episodes longer than kScanWin ticks are processed in windows with a
-// workgroup barrier between windows.
-constexpr int kScanThreads = 1024;
-
-constexpr int kScanWin = 4096;         // ticks resident per window (32 KB of rewards)
-constexpr int kReadySeg = 256;         // ticks per ready counter
+//   1. wave 0: chunk start states from a wave-level scan of the chunk maps;
+//      all waves: the episode's prefix words -> LDS (one coalesced pass);
+//   2. all waves: per tick, state = one field of its prefix word; gather the
+//      reward of that state into LDS, count trades;
+//   3. the rewards' sequential float64 sum, bit-exact (exact_ordered_sum).
+// Episodes longer than kScanWin ticks are processed in windows.
 
 template <int NSM>
 __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
@@ -463,8 +671,13 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
     double* sel = reinterpret_cast<double*>(lds);                          // [kScanWin]
     uint32_t* wl = reinterpret_cast<uint32_t*>(sel + kScanWin);            // [kScanWin]
     uint8_t* start = reinterpret_cast<uint8_t*>(wl + kScanWin);            // [nch]
-    __shared__ int ready[kScanWin / kReadySeg];
+    __shared__ double s_approx[kScanBlks];
+    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
+    __shared__ int32_t s_be[kScanBlks];
+    __shared__ uint64_t s_z[kScanBlks];
+    __shared__ uint8_t s_bad[kScanBlks];
     __shared__ int red_trades;
+    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
     const int nch = (T + kChunk - 1) / kChunk;
@@ -496,89 +709,35 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
     double total = 0.0;
     for (int w0 = 0; w0 < T; w0 += kScanWin) {
         const int n = min(kScanWin, T - w0);
-        // prefix words of the window -> LDS; clear the ready counters
         for (int i = tid; i < n; i += kScanThreads) wl[i] = words[so + w0 + i];
-        if (tid < kScanWin / kReadySeg) ready[tid] = 0;
         __syncthreads();
         SGMM_STAMP(e, 2);
-        if (tid >= kWave) {
-            // producers: wave w covers 64 consecutive ticks per pass (one ready
-            // segment), all of a thread's reward gathers issued before any write
-            constexpr int kPass = kScanThreads - kWave;  // 960 ticks per pass
-            constexpr int kMaxPass = (kScanWin + kPass - 1) / kPass;
-            const int i0 = tid - kWave;
+        {   // every reward gather of a thread issued before its first write
+            constexpr int kMaxPass = kScanWin / kScanThreads;
             double r[kMaxPass];
             uint32_t stv[kMaxPass], wdv[kMaxPass];
 #pragma unroll
-            for (int k = 0; k < kMaxPass; ++k) {
-                const int i = i0 + k * kPass;
+            for (int p = 0; p < kMaxPass; ++p) {
+                const int i = tid + p * kScanThreads;
                 if (i < n) {
-                    const int t = w0 + i;
-                    wdv[k] = wl[i];
-                    stv[k] = map_get(wdv[k], start[t / kChunk]);
-                    r[k] = rew[(so + t) * ns + stv[k]];
+                    wdv[p] = wl[i];
+                    stv[p] = map_get(wdv[p], start[(w0 + i) / kChunk]);
+                    r[p] = rew[(so + w0 + i) * ns + stv[p]];
                 }
             }
 #pragma unroll
-            for (int k = 0; k < kMaxPass; ++k) {
-                const int i = i0 + k * kPass;
-                if (k * kPass + (i0 & ~(kWave - 1)) >= n) break;  // whole wave past the end
-                const bool ok = i < n;
-                if (ok) {
-                    sel[i] = r[k];
-                    my_trades += (wdv[k] >> (24 + stv[k])) & 1u;
+            for (int p = 0; p < kMaxPass; ++p) {
+                const int i = tid + p * kScanThreads;
+                if (i < n) {
+                    sel[i] = r[p];
+                    my_trades += (wdv[p] >> (24 + stv[p])) & 1u;
                 }
-                const int cnt = __popcll(__ballot(ok));
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                if (lane == 0)
-                    __hip_atomic_fetch_add(&ready[(i & ~(kWave - 1)) / kReadySeg], cnt,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-        } else if (tid == 0) {
-            for (int sg = 0; sg * kReadySeg < n; ++sg) {
-                const int b = sg * kReadySeg, m = min(kReadySeg, n - b);
-                while (__hip_atomic_load(&ready[sg], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < m)
-                    __builtin_amdgcn_s_sleep(1);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                const double* buf = sel + b;
-                int t = 0;
-                if (m == kReadySeg) {
-                    // two 8-value register groups: LDS reads run 16 values ahead of the adds
-                    double2 a0 = *reinterpret_cast<const double2*>(buf + 0);
-                    double2 a1 = *reinterpret_cast<const double2*>(buf + 2);
-                    double2 a2 = *reinterpret_cast<const double2*>(buf + 4);
-                    double2 a3 = *reinterpret_cast<const double2*>(buf + 6);
-                    double2 b0 = *reinterpret_cast<const double2*>(buf + 8);
-                    double2 b1 = *reinterpret_cast<const double2*>(buf + 10);
-                    double2 b2 = *reinterpret_cast<const double2*>(buf + 12);
-                    double2 b3 = *reinterpret_cast<const double2*>(buf + 14);
-#pragma unroll 1
-                    for (t = 16; t < kReadySeg; t += 16) {
-                        total += a0.x; total += a0.y; total += a1.x; total += a1.y;
-                        total += a2.x; total += a2.y; total += a3.x; total += a3.y;
-                        a0 = *reinterpret_cast<const double2*>(buf + t);
-                        a1 = *reinterpret_cast<const double2*>(buf + t + 2);
-                        a2 = *reinterpret_cast<const double2*>(buf + t + 4);
-                        a3 = *reinterpret_cast<const double2*>(buf + t + 6);
-                        total += b0.x; total += b0.y; total += b1.x; total += b1.y;
-                        total += b2.x; total += b2.y; total += b3.x; total += b3.y;
-                        b0 = *reinterpret_cast<const double2*>(buf + t + 8);
-                        b1 = *reinterpret_cast<const double2*>(buf + t + 10);
-                        b2 = *reinterpret_cast<const double2*>(buf + t + 12);
-                        b3 = *reinterpret_cast<const double2*>(buf + t + 14);
-                    }
-                    total += a0.x; total += a0.y; total += a1.x; total += a1.y;
-                    total += a2.x; total += a2.y; total += a3.x; total += a3.y;
-                    total += b0.x; total += b0.y; total += b1.x; total += b1.y;
-                    total += b2.x; total += b2.y; total += b3.x; total += b3.y;
-                } else {
-                    for (; t < m; ++t) total += buf[t];
-                }
-                if (sg == 0) SGMM_STAMP(e, 3);
-            }
-            SGMM_STAMP(e, 4);
         }
         __syncthreads();
+        SGMM_STAMP(e, 3);
+        total = exact_ordered_sum<kScanThreads>(sel, n, total, sc);
+        SGMM_STAMP(e, 4);
     }
     SGMM_STAMP(e, 5);
     int wsum = my_trades;
@@ -592,6 +751,27 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
         fitness[e] = total;
         trades_out[e] = tr;
     }
+}
+
+// ------------------------------------------------------------------ ordered sum (standalone)
+// init + x[0] + x[1] + ... in sequential float64 order, one workgroup.
+__global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __restrict__ x, int64_t n,
+                                                              double init, double* __restrict__ out) {
+    __shared__ double sel[kScanWin];
+    __shared__ double s_approx[kScanBlks];
+    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
+    __shared__ int32_t s_be[kScanBlks];
+    __shared__ uint64_t s_z[kScanBlks];
+    __shared__ uint8_t s_bad[kScanBlks];
+    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
+    double S = init;
+    for (int64_t w0 = 0; w0 < n; w0 += kScanWin) {
+        const int m = (int)min((int64_t)kScanWin, n - w0);
+        for (int i = threadIdx.x; i < m; i += kScanThreads) sel[i] = x[w0 + i];
+        __syncthreads();
+        S = exact_ordered_sum<kScanThreads>(sel, m, S, sc);
+    }
+    if (threadIdx.x == 0) *out = S;
 }
 
 // ------------------------------------------------------------------ path scan (adversary)
@@ -883,7 +1063,7 @@ using namespace sgmm;
 
 #ifdef SGMM_STAMPS
 extern "C" int sgmm_debug_stamps(unsigned long long* host, int n_eps) {
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 8 * n_eps);
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * n_eps);
 }
 extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * n_waves);
@@ -943,6 +1123,17 @@ static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm
     else if (nsi <= 5) SGMM_TABLE(5, false);
     else SGMM_TABLE(8, false);
 #undef SGMM_TABLE
+}
+
+extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, double* out,
+                                void* stream) {
+    clear_error();
+    SGMM_REQUIRE(out && (values || n == 0) && n >= 0, "bad arguments");
+    ProfScope prof("ordered_sum", as_stream(stream));
+    hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
+                       init, out);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
 }
 
 extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes* eps,

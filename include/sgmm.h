@@ -242,6 +242,12 @@ int sgmm_ga_step(sgmm_ga_state *state, const double *fitness, const int32_t *tra
                  sgmm_ga_history *history, int32_t history_cap,
                  float *next_pop_mm, float *next_pop_adv, int32_t i0, int32_t n, void *stream);
 
+/* Sequential float64 sum init + values[0] + values[1] + ... (device array,
+ * result written to *out on the stream): the episode total of
+ * Env/drl_engine.py:53 (total_reward += reward), evaluated in parallel and
+ * bit-identical to the sequential loop.  The rollout uses the same routine. */
+int sgmm_ordered_sum(const double *values, int64_t n, double init, double *out, void *stream);
+
 /* Kernel timing for benchmarks / diagnostics (not on by default).
  * While enabled, every kernel the library launches is bracketed by a pair of
  * hipEvents recorded on its stream.  sgmm_profile_read waits for the recorded

@@ -249,3 +249,49 @@ def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
         for i, ep in enumerate(group):
             f, t = _oracle_eval(oracle, ep)
             assert trd[i].item() == t and fit[i].item() == f, (path, H, arl, i)
+
+
+def _seq_sum(init, x):
+    s = np.float64(init)
+    for v in np.asarray(x, np.float64):
+        s = s + v
+    return s
+
+
+def _sum_cases():
+    rng = np.random.default_rng(11)
+    tick = 2.0 ** -53
+    env_like = np.where(rng.random(4320) < 0.4, 0.0,
+                        np.where(rng.random(4320) < 0.5, -1e-4 * rng.integers(0, 3, 4320),
+                                 rng.normal(4e-4, 1e-3, 4320)))
+    ties = np.concatenate([[1.0], np.full(40, tick), [3 * tick, -tick, 2.0, 0.5 * tick], np.full(40, 3 * tick)])
+    cancel = np.array([1.0, -1.0, 1e-300, -1e-300, 0.0, -0.0, 2.5, -2.5, 1e-3] * 30)
+    subn = np.array([5e-324, 1e-310, -5e-324, 2.2250738585072014e-308, -1e-310] * 20)
+    wide = rng.choice([-1.0, 1.0], 3000) * 2.0 ** rng.uniform(-60, 40, 3000)
+    special = np.concatenate([rng.normal(0, 1, 100), [np.nan], rng.normal(0, 1, 50)])
+    infs = np.concatenate([rng.normal(0, 1, 100), [np.inf], rng.normal(0, 1, 50), [-np.inf]])
+    walk = rng.normal(1e-3, 2e-3, 100_000)
+    boundary = np.array([0.5, 0.25, 0.25, -0.5, 0.125, 0.125, 0.25, 1.0, -2.0, 2.0 ** -30] * 50)
+    return [("env_like", 0.0, env_like), ("ties", 0.0, ties), ("cancel", 0.0, cancel),
+            ("subnormal", 0.0, subn), ("wide", 0.0, wide), ("nan", 0.0, special),
+            ("inf", 0.0, infs), ("walk_100k", 0.0, walk), ("boundary", 0.0, boundary),
+            ("init", 0.1, env_like[:1000]), ("neg_init", -3.0, env_like[:2000]),
+            ("n0", 0.25, np.zeros(0)), ("n1", 0.0, np.array([0.3])), ("n15", 0.0, env_like[:15]),
+            ("n16", 0.0, env_like[:16]), ("n17", 0.0, env_like[:17]), ("n4097", 0.0, env_like[:4097] * 1e3)]
+
+
+@pytest.mark.parametrize("name,init,x", _sum_cases(), ids=[c[0] for c in _sum_cases()])
+def test_ordered_sum_matches_sequential(sgmm, name, init, x):
+    """The parallel exact episode sum equals total += r in float64, bit for bit."""
+    from sgmm_amd import _lib
+    L = _lib.load()
+    xd = torch.from_numpy(np.ascontiguousarray(x, np.float64)).to(DEV)
+    out = torch.zeros(1, dtype=torch.float64, device=DEV)
+    _lib.check(L.sgmm_ordered_sum(_lib.ptr(xd) if len(x) else None, len(x), float(init), _lib.ptr(out),
+                                  _lib.stream_ptr()), "ordered_sum")
+    got = out.cpu().numpy()[0]
+    want = _seq_sum(init, x)
+    if np.isnan(want):
+        assert np.isnan(got)
+    else:
+        assert got.tobytes() == np.float64(want).tobytes(), (name, got, want)

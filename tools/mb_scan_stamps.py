@@ -26,9 +26,13 @@ for P in (1, 64):
     for _ in range(3):
         eng.fitness(ticks, eps, params, pop, H)
     torch.cuda.synchronize()
-    h = np.zeros((P, 8), np.uint64)
+    h = np.zeros((P, 16), np.uint64)
     L.sgmm_debug_stamps(h.ctypes.data, P)
     d = (h[:, 1:6].astype(np.int64) - h[:, [0]].astype(np.int64))
     print(f"P={P}: cycles from kernel start (median over episodes): chunk-starts {np.median(d[:,0]):.0f}, "
-          f"words-in-LDS {np.median(d[:,1]):.0f}, first segment summed {np.median(d[:,2]):.0f}, "
-          f"all summed {np.median(d[:,3]):.0f}, end {np.median(d[:,4]):.0f}")
+          f"words-in-LDS {np.median(d[:,1]):.0f}, rewards gathered {np.median(d[:,2]):.0f}, "
+          f"sum done {np.median(d[:,3]):.0f}, end {np.median(d[:,4]):.0f}")
+    ds = (h[:, 8:13].astype(np.int64) - h[:, [0]].astype(np.int64))
+    print(f"   sum phases: approx sums {np.median(ds[:,0]):.0f}, approx starts {np.median(ds[:,1]):.0f}, "
+          f"int steps {np.median(ds[:,2]):.0f}, z-prefix {np.median(ds[:,3]):.0f}, walk {np.median(ds[:,4]):.0f}; "
+          f"walk iterations med {np.median(h[:,13]):.0f} max {h[:,13].max()}, slow blocks med {np.median(h[:,14]):.0f} max {h[:,14].max()}, slow-path cycles med {np.median(h[:,15]):.0f}, fast-part cycles med {np.median(h[:,7]):.0f}")
