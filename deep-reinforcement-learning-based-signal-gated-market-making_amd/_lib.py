@@ -53,7 +53,12 @@ class GAState(ctypes.Structure):
                 ("best_idx", ctypes.c_int32), ("adv_best_idx", ctypes.c_int32),
                 ("gen", ctypes.c_int32), ("improved", ctypes.c_int32),
                 ("decayed", ctypes.c_int32), ("patience", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("decay", ctypes.c_double)]
+                ("arrivals", ctypes.c_int32), ("decay", ctypes.c_double)]
+
+
+class AskedPopulation(ctypes.Structure):
+    _fields_ = [("state", ctypes.c_void_p), ("master_mm", ctypes.c_void_p), ("master_adv", ctypes.c_void_p),
+                ("seed", ctypes.c_uint64), ("i0", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 class GAHistory(ctypes.Structure):
@@ -91,6 +96,11 @@ SIGNATURES = {
     "sgmm_ga_step": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _I32, _I32, _I64, _VP, _VP, _VP, _I64, _I64, _U64,
                                     _VP, _I32, _VP, _VP, _I32, _I32, _VP]),
     "sgmm_ordered_sum": (ctypes.c_int, [_VP, _I64, ctypes.c_double, _VP, _VP]),
+    "sgmm_rollout_fitness_asked": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                                  ctypes.POINTER(AskedPopulation), _I32, _VP, _VP, _VP,
+                                                  ctypes.c_size_t, _VP]),
+    "sgmm_generation": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP, _VP, _VP, _VP, _VP,
+                                       _I32, _U64, _I32, _VP, _VP, _VP, _I32, _VP, ctypes.c_size_t, _VP]),
     "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "sgmm_profile_read": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
 }

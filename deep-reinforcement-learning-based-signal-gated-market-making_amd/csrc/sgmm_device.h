@@ -261,4 +261,48 @@ __device__ __forceinline__ void normal4(uint64_t seed, uint32_t stream_id, uint3
     z[3] = m1 * s1;
 }
 
+// ask() of one individual, 4 consecutive parameters (models/model.py:65-71).
+// out = master + (z * (float)sigma): the reference's randn_like * sigma in
+// float32, then the float32 add (model.py:69-70).
+__device__ __forceinline__ void ask_row4(const float* __restrict__ master, int64_t n_params,
+                                         float sig, uint64_t seed, uint32_t sid, uint32_t gen,
+                                         uint32_t indiv, int64_t k4, float* dst) {
+    float z[4];
+    normal4(seed, sid, gen, indiv, (uint32_t)k4, z);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t k = 4 * k4 + q;
+        if (k < n_params) {
+            const float noise = z[q] * sig;
+            dst[q] = master[k] + noise;
+        }
+    }
+}
+
+// first index of the maximum, NaN counting as the maximum (np.argmax)
+__device__ __forceinline__ bool better(double a, int ia, double b, int ib) {
+    const bool na = a != a, nb = b != b;
+    if (na != nb) return na;
+    if (na) return ia < ib;
+    if (a != b) return a > b;
+    return ia < ib;
+}
+
+// Population results gathered shard by shard: individual i's value lives in
+// shard i / n at byte offset (i / n) * stride, element i % n (n <= 0: one
+// contiguous array).  This is the layout of an all-gather of per-rank records.
+struct ShardView {
+    int32_t n;
+    int64_t stride;
+};
+
+template <class T>
+__device__ __forceinline__ T shard_at(const T* __restrict__ base, ShardView v, int i) {
+    if (v.n <= 0) return base[i];
+    const char* p = reinterpret_cast<const char*>(base) + (int64_t)(i / v.n) * v.stride;
+    return reinterpret_cast<const T*>(p)[i % v.n];
+}
+
+constexpr int kMaxStepParams = 4096;  // largest genome a one-workgroup GA step stages in LDS
+
 }  // namespace sgmm

@@ -7,27 +7,10 @@
 #include <cmath>
 
 #include "sgmm_device.h"
+#include "sgmm_ga_device.h"
 #include "sgmm_internal.h"
 
 namespace sgmm {
-
-// ask: one thread per 4 consecutive parameters of one individual.
-// out = master + (z * (float)sigma): the reference's randn_like * sigma in
-// float32, then the float32 add (model.py:69-70).
-__device__ __forceinline__ void ask_row4(const float* __restrict__ master, int64_t n_params,
-                                         float sig, uint64_t seed, uint32_t sid, uint32_t gen,
-                                         uint32_t indiv, int64_t k4, float* dst) {
-    float z[4];
-    normal4(seed, sid, gen, indiv, (uint32_t)k4, z);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int64_t k = 4 * k4 + q;
-        if (k < n_params) {
-            const float noise = z[q] * sig;
-            dst[q] = master[k] + noise;
-        }
-    }
-}
 
 __global__ void k_ga_ask(const float* __restrict__ master, int64_t n_params,
                          const sgmm_ga_state* __restrict__ st, uint32_t sid, uint64_t seed,
@@ -44,15 +27,6 @@ __global__ void k_ga_ask(const float* __restrict__ master, int64_t n_params,
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         if (4 * k4 + q < n_params) row[4 * k4 + q] = v[q];
-}
-
-// first index of the maximum, NaN counting as the maximum (np.argmax)
-__device__ __forceinline__ bool better(double a, int ia, double b, int ib) {
-    const bool na = a != a, nb = b != b;
-    if (na != nb) return na;
-    if (na) return ia < ib;
-    if (a != b) return a > b;
-    return ia < ib;
 }
 
 constexpr int kTellBlock = 256;
@@ -187,86 +161,8 @@ __global__ void k_ga_state_init(sgmm_ga_state* st, double sigma, int32_t patienc
     st->improved = 0;
     st->decayed = 0;
     st->patience = patience;
-    st->pad_ = 0;
+    st->arrivals = 0;
     st->decay = decay;
-}
-
-// ---------------------------------------------------------------- fused boundary
-constexpr int kStepBlock = 1024;
-constexpr int kMaxStepParams = 4096;  // master staged in LDS
-
-// Population results gathered shard by shard: individual i's value lives in
-// shard i / n at byte offset (i / n) * stride, element i % n (n <= 0: one
-// contiguous array).  This is the layout of an all-gather of per-rank records.
-struct ShardView {
-    int32_t n;
-    int64_t stride;
-};
-
-template <class T>
-__device__ __forceinline__ T shard_at(const T* __restrict__ base, ShardView v, int i) {
-    if (v.n <= 0) return base[i];
-    const char* p = reinterpret_cast<const char*>(base) + (int64_t)(i / v.n) * v.stride;
-    return reinterpret_cast<const T*>(p)[i % v.n];
-}
-
-__device__ void block_argmax2(const double* __restrict__ fit, ShardView sv_, int P, int& best,
-                              int& abest, double* sv, int* si) {
-    const int tid = threadIdx.x, nt = blockDim.x;
-    double bv = 0.0, av = 0.0;
-    int bi = -1, aj = -1;
-    for (int i = tid; i < P; i += nt) {
-        const double f = shard_at(fit, sv_, i);
-        if (bi < 0 || better(f, i, bv, bi)) { bv = f; bi = i; }
-        if (aj < 0 || better(-f, i, av, aj)) { av = -f; aj = i; }
-    }
-    sv[tid] = bv; si[tid] = bi;
-    sv[nt + tid] = av; si[nt + tid] = aj;
-    __syncthreads();
-    for (int w = nt / 2; w > 0; w >>= 1) {
-        if (tid < w) {
-#pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int o = r * nt;
-                const int io = si[o + tid + w];
-                if (io >= 0 && (si[o + tid] < 0 || better(sv[o + tid + w], io, sv[o + tid], si[o + tid]))) {
-                    sv[o + tid] = sv[o + tid + w];
-                    si[o + tid] = io;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    best = si[0];
-    abest = si[nt];
-}
-
-// master <- ask(best) in place; staged copy to LDS for the next ask
-__device__ void regen_master(float* __restrict__ master, float* lds_master, int64_t n, float sig,
-                             uint64_t seed, uint32_t sid, uint32_t gen, int best) {
-    for (int64_t k4 = threadIdx.x; k4 < (n + 3) / 4; k4 += blockDim.x) {
-        float v[4];
-        ask_row4(master, n, sig, seed, sid, gen, (uint32_t)best, k4, v);
-        for (int q = 0; q < 4; ++q)
-            if (4 * k4 + q < n) {
-                master[4 * k4 + q] = v[q];
-                lds_master[4 * k4 + q] = v[q];
-            }
-    }
-}
-
-__device__ void ask_rows(const float* lds_master, int64_t n, float sig, uint64_t seed,
-                         uint32_t sid, uint32_t gen, int32_t i0, int32_t cnt,
-                         float* __restrict__ out) {
-    const int64_t nk4 = (n + 3) / 4;
-    for (int64_t g = threadIdx.x; g < nk4 * cnt; g += blockDim.x) {
-        const int32_t i = (int32_t)(g / nk4);
-        const int64_t k4 = g - (int64_t)i * nk4;
-        float v[4];
-        ask_row4(lds_master, n, sig, seed, sid, gen, (uint32_t)(i0 + i), k4, v);
-        for (int q = 0; q < 4; ++q)
-            if (4 * k4 + q < n) out[(int64_t)i * n + 4 * k4 + q] = v[q];
-    }
 }
 
 __global__ __launch_bounds__(kStepBlock) void k_ga_step(
@@ -280,60 +176,8 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
     __shared__ int si[2 * kStepBlock];
     __shared__ float lm[kMaxStepParams];
     __shared__ float la[kMaxStepParams];
-    __shared__ int improved;
-    __shared__ float next_sig[2];
-    const int tid = threadIdx.x;
-    const uint32_t gen = (uint32_t)st->gen;
-    sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
-    int best, abest;
-    block_argmax2(fit, shard, P, best, abest, sv, si);
-    const float sig_mm = (float)st->sigma_mm, sig_adv = (float)st->sigma_adv;
-    __syncthreads();
-    // tell (model.py:73-76; drl_engine.py:119-125)
-    regen_master(master, lm, n_mm, sig_mm, seed, 0u, gen, best);
-    if (master_adv) regen_master(master_adv, la, n_adv, sig_adv, seed, 1u, gen, abest);
-    if (tid == 0) {
-        // validation of the best (drl_engine.py:129-171)
-        const double v = shard_at(vfit, shard, best);
-        improved = v > st->best_val;
-        int decayed = 0;
-        if (improved) {
-            st->best_val = v;
-            st->no_improve = 0;
-        } else {
-            st->no_improve += 1;
-        }
-        if (st->no_improve >= st->patience) {
-            st->sigma_mm *= st->decay;
-            st->sigma_adv *= st->decay;
-            st->no_improve = 0;
-            decayed = 1;
-        }
-        st->best_idx = best;
-        st->adv_best_idx = abest;
-        st->last_train_f = shard_at(fit, shard, best);
-        st->improved = improved;
-        st->decayed = decayed;
-        st->last_val_f = v;
-        st->gen += 1;
-        next_sig[0] = (float)st->sigma_mm;
-        next_sig[1] = (float)st->sigma_adv;
-        if (hist) {
-            hist->train_f = shard_at(fit, shard, best);
-            hist->train_trades = trades ? shard_at(trades, shard, best) : 0;
-            hist->best_idx = best;
-            hist->val_f = v;
-            hist->val_trades = vtrades ? shard_at(vtrades, shard, best) : 0;
-            hist->sigma_after = st->sigma_mm;
-            hist->flags = improved | (decayed << 1);
-        }
-    }
-    __syncthreads();
-    if (improved && best_master)
-        for (int64_t k = tid; k < n_mm; k += kStepBlock) best_master[k] = lm[k];
-    // ask of the next generation (model.py:65-71) from the new master / sigma
-    if (next_mm) ask_rows(lm, n_mm, next_sig[0], seed, 0u, gen + 1, i0, n, next_mm);
-    if (next_adv && master_adv) ask_rows(la, n_adv, next_sig[1], seed, 1u, gen + 1, i0, n, next_adv);
+    ga_step_dev(st, fit, trades, vfit, vtrades, P, shard, master, master_adv, best_master, n_mm,
+                n_adv, seed, history, hist_cap, next_mm, next_adv, i0, n, sv, si, lm, la);
 }
 
 }  // namespace sgmm

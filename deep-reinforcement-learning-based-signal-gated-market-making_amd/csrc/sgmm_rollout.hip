@@ -28,10 +28,12 @@
 // Trace path (sgmm_rollout_trace): k_rollout_direct, one wave per episode,
 // lane = hidden neuron, the literal step loop (independent second
 // implementation; the tests require both paths to agree bit for bit).
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
 #include "sgmm_device.h"
+#include "sgmm_ga_device.h"
 #include "sgmm_internal.h"
 
 namespace sgmm {
@@ -49,6 +51,59 @@ struct EpArrays {
     const int64_t* step_off;
     const int32_t* param;
 };
+
+// Where an episode's genomes come from: materialized rows (pop != nullptr) or
+// the current generation's ask() of the GA state, generated in the kernel
+// (never written to memory): individual i0 + genome[e], values identical to
+// what sgmm_ga_ask writes.
+struct GenomeSrc {
+    const float* mm;
+    int64_t mm_stride;
+    const float* adv;
+    int64_t adv_stride;
+    const sgmm_ga_state* st;
+    const float* master_mm;
+    const float* master_adv;
+    uint64_t seed;
+    int32_t i0;
+};
+
+constexpr int kAdvParams = 74;  // AdversaryPolicy weights = first 74 floats of the genome
+
+// Stage the policy genome (n floats) of individual gi and, when ga != nullptr
+// and ai >= 0, the adversary weights of individual ai into LDS.  Every thread
+// of the block calls; the caller synchronizes.
+__device__ void stage_genomes(const GenomeSrc& src, int gi, int ai, int n, float* gs, float* ga) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (src.st) {
+        const uint32_t gen = (uint32_t)src.st->gen;
+        const float sig = (float)src.st->sigma_mm;
+        for (int k4 = tid; k4 < (n + 3) / 4; k4 += nt) {
+            float v[4];
+            ask_row4(src.master_mm, n, sig, src.seed, 0u, gen, (uint32_t)(src.i0 + gi), k4, v);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * k4 + q < n) gs[4 * k4 + q] = v[q];
+        }
+        if (ga && ai >= 0) {
+            const float siga = (float)src.st->sigma_adv;
+            for (int k4 = tid; k4 < (kAdvParams + 3) / 4; k4 += nt) {
+                float v[4];
+                ask_row4(src.master_adv, kAdvParams, siga, src.seed, 1u, gen, (uint32_t)(src.i0 + ai), k4, v);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (4 * k4 + q < kAdvParams) ga[4 * k4 + q] = v[q];
+            }
+        }
+    } else {
+        const float* __restrict__ row = src.mm + (int64_t)gi * src.mm_stride;
+        for (int k = tid; k < n; k += nt) gs[k] = row[k];
+        if (ga && ai >= 0) {
+            const float* __restrict__ arow = src.adv + (int64_t)ai * src.adv_stride;
+            for (int k = tid; k < kAdvParams; k += nt) ga[k] = arow[k];
+        }
+    }
+}
 
 // ------------------------------------------------------------------ transition maps
 // A step's effect on the (<= 8) inventory states is a map state -> state,
@@ -90,8 +145,7 @@ __device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
 template <int H, int NSM, bool ARL>
 __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
-    const float* __restrict__ mm, int64_t mm_stride, const float* __restrict__ adv,
-    int64_t adv_stride, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    GenomeSrc src, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
     uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
@@ -100,7 +154,11 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     const int w = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const int ns = ARL ? 4 * nsi : nsi;
     const sgmm_env_params p = params[ep.param[e]];
-    const float* __restrict__ g = mm + (int64_t)ep.genome[e] * mm_stride;
+    __shared__ float gsm[GenomeLayout<H>::N];
+    __shared__ float gsa[kAdvParams];
+    const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
+    stage_genomes(src, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
+    const float* g = gsm;
 
     __shared__ float sx[2][kChunk];
     __shared__ double spx[5][kChunk];
@@ -123,14 +181,12 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
             }
         }
     }
+    __syncthreads();  // staged genomes
     if (ARL) {
-        const int ai = ep.adv ? ep.adv[e] : -1;
         if ((int)threadIdx.x < ns) {
             const int s = threadIdx.x;
             int32_t da = 0, db = 0;
-            if (ai >= 0)
-                adv_delta(adv + (int64_t)ai * adv_stride, p, inv_min + (s >> 2), (s >> 1) & 1,
-                          s & 1, da, db);
+            if (ai >= 0) adv_delta(gsa, p, inv_min + (s >> 2), (s >> 1) & 1, s & 1, da, db);
             lut[0][s] = da;
             lut[1][s] = db;
         }
@@ -251,12 +307,12 @@ __device__ unsigned long long g_tstamps[8192][8];
 //                    2-row output would waste 7/8 of a 16-row MFMA tile).
 // The lane then holds the policy outputs of its own tick for every state.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int H, int NSI, bool ARL>
-__global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
+__global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfma(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
-    const float* __restrict__ mm, int64_t mm_stride, const float* __restrict__ adv,
-    int64_t adv_stride, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    GenomeSrc src, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
     uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     static_assert(H % 16 == 0, "MFMA table needs H multiple of 16");
     using L = GenomeLayout<H>;
@@ -267,16 +323,40 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     const int32_t T = ep.len[e];
     const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int32_t t0 = chunk * kChunk;
-    if (t0 >= T) return;  // wave-uniform; no block barriers below
+    if (blockIdx.x * 4 * kChunk >= T) return;  // block-uniform: no wave of this block has ticks
     const int lane = threadIdx.x & (kWave - 1), grp = lane >> 4, col = lane & 15;
     const int ns = ARL ? 4 * nsi : nsi;
+    // this wave's tick data, requested before the genome staging so the loads
+    // overlap it (indices clamped into the episode: padded samples are discarded)
+    float xs0[4], xs1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t ti = ep.tick_off[e] + min(t0 + 16 * q + col, T - 1);
+        xs0[q] = tk.s1n[ti];
+        xs1[q] = tk.s2n[ti];
+    }
+    const int64_t tix = ep.tick_off[e] + min(t0 + lane, T - 1);
+    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
+    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
+    // the episode's genomes -> LDS (all four waves, before any of them leaves)
+    __shared__ __attribute__((aligned(16))) float gsm[GenomeLayout<H>::N];
+    __shared__ float gsa[kAdvParams];
+    const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
+    stage_genomes(src, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
+    __syncthreads();
+    // layer-3 weights interleaved (W3[0][j], W3[1][j]) for the packed output chains
+    __shared__ __attribute__((aligned(8))) float w3i[2 * H];
+    if (threadIdx.x < 2 * H)
+        w3i[threadIdx.x] = gsm[GenomeLayout<H>::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
+    __syncthreads();
+    if (t0 >= T) return;  // wave-uniform; no block barriers below
 #ifdef SGMM_STAMPS
     const int wslot = e * (int)(gridDim.x * 4) + chunk;
 #endif
     SGMM_TSTAMP_REAL(wslot, 7);
     SGMM_TSTAMP(wslot, 0, 0);
     const sgmm_env_params p = params[ep.param[e]];
-    const float* __restrict__ g = mm + (int64_t)ep.genome[e] * mm_stride;
+    const float* g = gsm;
     const int64_t row = ep.step_off[e] + t0 + lane;  // this lane's output row
     __shared__ __attribute__((aligned(16))) float hb_s[4][kWave * HP];
     float* hb = hb_s[threadIdx.x >> 6];
@@ -294,14 +374,6 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     float w1s[KS];      // layer-1 inventory weight W1[k][2] for k = 4i + grp
     float pre[4][KS];   // b1[k] + W1[k][0] s1n + W1[k][1] s2n of sample 16q + col
     {
-        float xs0[4], xs1[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int tq = min(t0 + 16 * q + col, T - 1);  // clamp: padded samples are discarded
-            const int64_t ti = ep.tick_off[e] + tq;
-            xs0[q] = tk.s1n[ti];
-            xs1[q] = tk.s2n[ti];
-        }
 #pragma unroll
         for (int i = 0; i < KS; ++i) {
             const int k = 4 * i + grp;
@@ -311,11 +383,6 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
             for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(a1, xs1[q], __builtin_fmaf(a0, xs0[q], bb));
         }
     }
-    // this lane's tick record for the FPT step, fetched now so its latency
-    // hides under the policy evaluation
-    const int64_t tix = ep.tick_off[e] + min(t0 + lane, T - 1);
-    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
-    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
     SGMM_TSTAMP(wslot, 1, w2f[0][0] + w1s[KS - 1] + pre[3][KS - 1] + b2c[0][0]);
 
     // ---- the policy for every (state, tick) of the chunk
@@ -330,15 +397,20 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int rt = 0; rt < NT; ++rt) acc[q][rt] = b2c[rt];
-        // four independent 16-sample chains, issued interleaved (k-step outer)
+        // four independent 16-sample chains, issued interleaved (k-step outer);
+        // layer 1's last term for two tiles per packed fma
 #pragma unroll
         for (int i = 0; i < KS; ++i)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+            for (int q = 0; q < 4; q += 2) {
+                const f32x2 hh = __builtin_elementwise_fma(f32x2{w1s[i], w1s[i]}, f32x2{x2, x2},
+                                                           f32x2{pre[q][i], pre[q + 1][i]});
+                const float h1a = relu(hh.x), h1b = relu(hh.y);
 #pragma unroll
-                for (int rt = 0; rt < NT; ++rt)
-                    acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, acc[q][rt], 0, 0, 0);
+                for (int rt = 0; rt < NT; ++rt) {
+                    acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1a, acc[q][rt], 0, 0, 0);
+                    acc[q + 1][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1b, acc[q + 1][rt], 0, 0, 0);
+                }
             }
         // transpose relu(H2) through LDS: lane n gets tick n's H activations
 #pragma unroll
@@ -351,18 +423,18 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
                 *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
             }
         __builtin_amdgcn_wave_barrier();
-        float o0 = g[L::B3], o1 = g[L::B3 + 1];
+        f32x2 o = {g[L::B3], g[L::B3 + 1]};  // both output chains in one packed fma per neuron
 #pragma unroll
         for (int j4 = 0; j4 < H / 4; ++j4) {
             const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                o0 = __builtin_fmaf(g[L::W3 + 4 * j4 + r], h[r], o0);
-                o1 = __builtin_fmaf(g[L::W3 + H + 4 * j4 + r], h[r], o1);
+                const f32x2 w = *reinterpret_cast<const f32x2*>(&w3i[2 * (4 * j4 + r)]);
+                o = __builtin_elementwise_fma(w, f32x2{h[r], h[r]}, o);
             }
         }
-        out0[si] = o0;
-        out1[si] = o1;
+        out0[si] = o.x;
+        out1[si] = o.y;
         __builtin_amdgcn_wave_barrier();
     }
     SGMM_TSTAMP(wslot, 2, out0[NSI - 1] + out1[0]);
@@ -373,12 +445,9 @@ __global__ __launch_bounds__(kWave * 4) void k_policy_table_mfma(
     int32_t* lut0 = lut_s[threadIdx.x >> 6][0];
     int32_t* lut1 = lut_s[threadIdx.x >> 6][1];
     if (ARL) {
-        const int ai = ep.adv ? ep.adv[e] : -1;
         if (lane < ns) {
             int32_t da = 0, db = 0;
-            if (ai >= 0)
-                adv_delta(adv + (int64_t)ai * adv_stride, p, inv_min + (lane >> 2), (lane >> 1) & 1,
-                          lane & 1, da, db);
+            if (ai >= 0) adv_delta(gsa, p, inv_min + (lane >> 2), (lane >> 1) & 1, lane & 1, da, db);
             lut0[lane] = da;
             lut1[lane] = db;
         }
@@ -652,6 +721,57 @@ __device__ double exact_ordered_sum(const double* sel, int n, double S, SumScrat
     return S;
 }
 
+// ------------------------------------------------------------------ generation tail
+// A fitness launch can end the generation itself: every workgroup publishes
+// its episode's result (agent-scope release, arrival ticket); the last one to
+// arrive acquires, runs the GA step (tell, validation bookkeeping, sigma
+// decay, history) and resets the ticket.  Saves the separate GA launch.
+struct StepArgs {
+    sgmm_ga_state* st;  // nullptr: no GA step in this launch
+    float* master_mm;
+    float* master_adv;
+    float* best_master;
+    int64_t n_mm, n_adv;
+    uint64_t seed;
+    sgmm_ga_history* history;
+    int32_t hist_cap;
+    int32_t P;          // fitness[0..P): training, fitness[P..2P): validation
+};
+
+// LDS bytes the tail needs (aliased onto the kernel's dynamic LDS)
+static inline size_t step_lds_bytes(int threads, const StepArgs& sa) {
+    return (size_t)threads * 2 * (sizeof(double) + sizeof(int)) +
+           sizeof(float) * (size_t)(sa.n_mm + (sa.master_adv ? sa.n_adv : 0));
+}
+
+__device__ void generation_tail(const StepArgs& sa, const double* fitness, const int32_t* trades,
+                                unsigned char* lds, int* s_last) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(&sa.st->arrivals, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = prev == (int)gridDim.x - 1;
+        if (*s_last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    const int nt = blockDim.x;
+    double* sv = reinterpret_cast<double*>(lds);
+    int* si = reinterpret_cast<int*>(sv + 2 * nt);
+    float* lm = reinterpret_cast<float*>(si + 2 * nt);
+    float* la = lm + sa.n_mm;
+    ga_step_dev(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, ShardView{0, 0},
+                sa.master_mm, sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed, sa.history,
+                sa.hist_cap, nullptr, nullptr, 0, 0, sv, si, lm, la);
+    if (threadIdx.x == 0) sa.st->arrivals = 0;
+}
+
 // ------------------------------------------------------------------ path scan (no adversary)
 // One workgroup (16 waves) per episode.
 //   1. wave 0: chunk start states from a wave-level scan of the chunk maps;
@@ -666,7 +786,7 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
     const uint32_t* __restrict__ words, const uint32_t* __restrict__ cmaps,
     const double* __restrict__ rew, double* __restrict__ fitness,
-    int32_t* __restrict__ trades_out) {
+    int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);                          // [kScanWin]
     uint32_t* wl = reinterpret_cast<uint32_t*>(sel + kScanWin);            // [kScanWin]
@@ -751,6 +871,7 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
         fitness[e] = total;
         trades_out[e] = tr;
     }
+    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
 }
 
 // ------------------------------------------------------------------ ordered sum (standalone)
@@ -786,9 +907,15 @@ __device__ __forceinline__ int next_state_arl(int s, int code) {
 __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
     const uint64_t* __restrict__ fills, const double* __restrict__ rew,
-    double* __restrict__ fitness, int32_t* __restrict__ trades_out) {
+    double* __restrict__ fitness, int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);
+    __shared__ double s_approx[kScanBlks];
+    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
+    __shared__ int32_t s_be[kScanBlks];
+    __shared__ uint64_t s_z[kScanBlks];
+    __shared__ uint8_t s_bad[kScanBlks];
+    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
     const int ns = 4 * nsi;
@@ -834,9 +961,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
             }
         }
         __syncthreads();
-        if (tid == 0)
-            for (int t = 0; t < segn; ++t) total += sel[t];
-        __syncthreads();
+        total = exact_ordered_sum<kScanBlock>(sel, segn, total, sc);
     }
     int w = my_trades;
 #pragma unroll
@@ -849,6 +974,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
         fitness[e] = total;
         trades_out[e] = tr;
     }
+    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
 }
 
 // ------------------------------------------------------------------ direct (trace) path
@@ -1091,14 +1217,13 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
 template <int H>
 static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
                               const sgmm_ticks& tk, const EpArrays& ep,
-                              const sgmm_env_params* params, const float* mm, int64_t mm_stride,
-                              const float* adv, int64_t adv_stride, int32_t inv_min,
+                              const sgmm_env_params* params, const GenomeSrc& src, int32_t inv_min,
                               uint32_t* words, uint32_t* cmaps, uint64_t* fills, double* rew) {
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
 #define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
     hipLaunchKernelGGL((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
-                       mm, mm_stride, adv, adv_stride, inv_min, nsi, words, cmaps, fills, rew)
+                       src, inv_min, nsi, words, cmaps, fills, rew)
     if (arl) {
         if (nsi <= 5) SGMM_TABLE_MFMA(5, true);
         else SGMM_TABLE_MFMA(8, true);
@@ -1112,13 +1237,13 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
 
 template <int H>
 static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm_ticks& tk,
-                         const EpArrays& ep, const sgmm_env_params* params, const float* mm,
-                         int64_t mm_stride, const float* adv, int64_t adv_stride, int32_t inv_min,
-                         uint32_t* words, uint32_t* cmaps, uint64_t* fills, double* rew) {
+                         const EpArrays& ep, const sgmm_env_params* params, const GenomeSrc& src,
+                         int32_t inv_min, uint32_t* words, uint32_t* cmaps, uint64_t* fills,
+                         double* rew) {
     const dim3 block(kChunk * nsi);  // one wave per inventory state
 #define SGMM_TABLE(NSM_, ARL_)                                                                  \
-    hipLaunchKernelGGL((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, mm,  \
-                       mm_stride, adv, adv_stride, inv_min, nsi, words, cmaps, fills, rew)
+    hipLaunchKernelGGL((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, src, \
+                       inv_min, nsi, words, cmaps, fills, rew)
     if (arl) SGMM_TABLE(8, true);
     else if (nsi <= 5) SGMM_TABLE(5, false);
     else SGMM_TABLE(8, false);
@@ -1136,17 +1261,12 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
     return SGMM_OK;
 }
 
-extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes* eps,
-                                    const sgmm_env_params* params, const float* mm_genomes,
-                                    int64_t mm_stride, int32_t hidden, const float* adv_genomes,
-                                    int64_t adv_stride, double* fitness, int32_t* trades,
-                                    void* workspace, size_t workspace_bytes, void* stream) {
-    clear_error();
-    if (int rc = check_episodes(ticks, eps, params, mm_genomes, hidden)) return rc;
+// table + path scan (+ the generation tail when step.st) for one batch
+static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                        const sgmm_env_params* params, const GenomeSrc& src, bool arl,
+                        int32_t hidden, double* fitness, int32_t* trades, void* workspace,
+                        size_t workspace_bytes, const StepArgs& step, hipStream_t s) {
     SGMM_REQUIRE(fitness && trades, "null fitness/trades output");
-    SGMM_REQUIRE(mm_stride >= (int64_t)hidden * hidden + 7 * hidden + 2, "mm_stride too small");
-    const bool arl = adv_genomes != nullptr;
-    SGMM_REQUIRE(!arl || adv_stride >= 74, "adv_stride < 74");
     if (eps->n == 0) return SGMM_OK;
     const int32_t nsi = eps->inv_max - eps->inv_min + 1;
     const int32_t ns = arl ? 4 * nsi : nsi;
@@ -1169,25 +1289,24 @@ extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes
         rew = reinterpret_cast<double*>(w + ws_words(eps->total_steps) +
                                         ws_cmaps(eps->n, eps->total_steps));
     }
-    hipStream_t s = as_stream(stream);
     const EpArrays ep = ep_arrays(eps, arl);
     if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof("policy_table", s);
         const bool valu = table_path() == 1;
         switch (hidden) {
-            case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew); break;
+            case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew); break;
             case 16:
-                if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
                 break;
             case 32:
-                if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
                 break;
             default:
-                if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<64>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                else launch_table_mfma<64>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
                 break;
         }
         SGMM_LAUNCHED();
@@ -1195,20 +1314,72 @@ extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes
     const int nch_max = (eps->max_len + kChunk - 1) / kChunk;
     ProfScope prof("path_scan", s);
     if (arl) {
-        const size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
+        size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
+        if (step.st) lds = std::max(lds, step_lds_bytes(kScanBlock, step));
         hipLaunchKernelGGL(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
-                           eps->inv_min, nsi, fills, rew, fitness, trades);
+                           eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
-        const size_t lds = kScanWin * (sizeof(double) + sizeof(uint32_t)) + nch_max;
+        size_t lds = kScanWin * (sizeof(double) + sizeof(uint32_t)) + nch_max;
+        if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
         if (nsi <= 5)
             hipLaunchKernelGGL(k_path_scan_maps<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades);
+                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
         else
             hipLaunchKernelGGL(k_path_scan_maps<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades);
+                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
     }
     SGMM_LAUNCHED();
     return SGMM_OK;
+}
+
+extern "C" int sgmm_rollout_fitness(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                                    const sgmm_env_params* params, const float* mm_genomes,
+                                    int64_t mm_stride, int32_t hidden, const float* adv_genomes,
+                                    int64_t adv_stride, double* fitness, int32_t* trades,
+                                    void* workspace, size_t workspace_bytes, void* stream) {
+    clear_error();
+    if (int rc = check_episodes(ticks, eps, params, mm_genomes, hidden)) return rc;
+    SGMM_REQUIRE(mm_stride >= (int64_t)hidden * hidden + 7 * hidden + 2, "mm_stride too small");
+    const bool arl = adv_genomes != nullptr;
+    SGMM_REQUIRE(!arl || adv_stride >= kAdvParams, "adv_stride < 74");
+    const GenomeSrc src{mm_genomes, mm_stride, adv_genomes, adv_stride, nullptr, nullptr, nullptr, 0, 0};
+    return rollout_impl(ticks, eps, params, src, arl, hidden, fitness, trades, workspace,
+                        workspace_bytes, StepArgs{}, as_stream(stream));
+}
+
+extern "C" int sgmm_rollout_fitness_asked(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                                          const sgmm_env_params* params,
+                                          const sgmm_asked_population* pop, int32_t hidden,
+                                          double* fitness, int32_t* trades, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(pop && pop->state && pop->master_mm, "null asked population");
+    if (int rc = check_episodes(ticks, eps, params, pop->master_mm, hidden)) return rc;
+    SGMM_REQUIRE(pop->i0 >= 0, "negative i0");
+    const bool arl = pop->master_adv != nullptr;
+    const GenomeSrc src{nullptr, 0, nullptr, 0, pop->state, pop->master_mm, pop->master_adv, pop->seed, pop->i0};
+    return rollout_impl(ticks, eps, params, src, arl, hidden, fitness, trades, workspace,
+                        workspace_bytes, StepArgs{}, as_stream(stream));
+}
+
+extern "C" int sgmm_generation(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                               const sgmm_env_params* params, sgmm_ga_state* state, float* master_mm,
+                               float* master_adv, float* best_master, int32_t hidden, uint64_t seed,
+                               int32_t P, double* fitness, int32_t* trades, sgmm_ga_history* history,
+                               int32_t history_cap, void* workspace, size_t workspace_bytes,
+                               void* stream) {
+    clear_error();
+    SGMM_REQUIRE(state && master_mm, "null state / master");
+    if (int rc = check_episodes(ticks, eps, params, master_mm, hidden)) return rc;
+    SGMM_REQUIRE(P > 0 && eps->n == 2 * P, "episodes must be P training + P validation episodes");
+    const int64_t n_mm = (int64_t)hidden * hidden + 7 * hidden + 2;
+    SGMM_REQUIRE(n_mm <= kMaxStepParams, "genome too large for the fused GA step");
+    const bool arl = master_adv != nullptr;
+    const GenomeSrc src{nullptr, 0, nullptr, 0, state, master_mm, master_adv, seed, 0};
+    StepArgs step{state, master_mm, master_adv, best_master, n_mm, arl ? 1250 : 0, seed, history,
+                  history_cap, P};
+    return rollout_impl(ticks, eps, params, src, arl, hidden, fitness, trades, workspace,
+                        workspace_bytes, step, as_stream(stream));
 }
 
 extern "C" int sgmm_rollout_trace(const sgmm_ticks* ticks, const sgmm_episodes* eps,

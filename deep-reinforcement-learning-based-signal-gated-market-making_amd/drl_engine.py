@@ -13,6 +13,7 @@ raise -- there is no CPU fallback.
 """
 from __future__ import annotations
 
+import ctypes
 import hashlib
 import os
 import sys
@@ -22,7 +23,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import GAHistory, GAState, check, ptr, stream_ptr
+from ._lib import AskedPopulation, GAHistory, GAState, check, ptr, stream_ptr
 from .model import NeuroEvolution, TradingPolicy, genome_size, genome_to_state_dict, hidden_from_genome
 from .rollout import EnvConfig, EpisodeBatch, RolloutEngine, TickStore, params_tensor
 from .shard import FitnessRecords, shard_bounds, shard_capacity  # noqa: F401 (re-exported)
@@ -250,27 +251,27 @@ class TrainingSession:
         g_tr, o_tr, l_tr = phase(tr_off, self.T_tr)
         g_va, o_va, l_va = phase(va_off, self.T_va)
         self.rec = FitnessRecords(P, self.world, dev)
-        if self.fused and not arl:  # one launch: training + validation episodes of the shard
+        if self.fused:  # one launch: training + validation episodes of the shard
+            adv = np.concatenate([g_tr, np.full(n_cap, -1)]) if arl else None  # validation: no adversary
             self.train_eps = EpisodeBatch(np.concatenate([g_tr, g_va]), np.concatenate([o_tr, o_va]),
-                                          np.concatenate([l_tr, l_va]), np.zeros(2 * n_cap)).to(dev)
+                                          np.concatenate([l_tr, l_va]), np.zeros(2 * n_cap), adv=adv).to(dev)
             self.val_eps = None
             self.out, self.vout = self.rec.both, None
         else:
             self.train_eps = EpisodeBatch(g_tr, o_tr, l_tr, np.zeros(n_cap),
                                           adv=g_tr if arl else None).to(dev)
             self.out = self.rec.train
-            if self.fused:
-                self.val_eps = EpisodeBatch(g_va, o_va, l_va, np.zeros(n_cap)).to(dev)
-                self.vout = self.rec.val
-            else:  # validation of the best only (reference order)
-                self.val_eps = EpisodeBatch(np.zeros(1), np.full(1, va_off), np.full(1, self.T_va),
-                                            np.zeros(1)).to(dev)
-                self.vout = (torch.empty(1, dtype=torch.float64, device=dev),
-                             torch.empty(1, dtype=torch.int32, device=dev))
+            # validation of the best only (reference order)
+            self.val_eps = EpisodeBatch(np.zeros(1), np.full(1, va_off), np.full(1, self.T_va),
+                                        np.zeros(1)).to(dev)
+            self.vout = (torch.empty(1, dtype=torch.float64, device=dev),
+                         torch.empty(1, dtype=torch.int32, device=dev))
         f32 = dict(dtype=torch.float32, device=dev)
         # population rows: the full population when the host draws it (torch
         # RNG), else the shard's capacity (pads point at row 0, which exists)
         n_rows = P if self.torch_rng else max(n_cap, 1)
+        if not self.torch_rng and self.fused and G <= 4096:
+            n_rows = 1  # asked population: generated inside the rollout (placeholder row)
         self.pop = torch.empty((n_rows, G), **f32)
         lo = min(self.i0, P - 1)
         self.pop_loc = self.pop[lo:lo + max(n_cap, 1)] if self.torch_rng else self.pop
@@ -285,12 +286,13 @@ class TrainingSession:
             raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
         check(self.L.sgmm_ga_state_init(ptr(self.state), float(eng.mm_evolver.sigma), eng.patience,
                                         eng.decay, stream_ptr()), "sgmm_ga_state_init")
-        # generation boundary in one launch (tell + validation + next ask) when the
-        # population is drawn on device and validated in the training launch
-        self.fast_step = (not self.torch_rng and self.fused and G <= 4096 and ADV_GENOME <= 4096
-                          and n_cap * G <= (1 << 22))
-        if self.fast_step:  # the ask of generation 0; later asks follow each ga_step
-            self._ask()
+        # device RNG + fused validation: the population is never materialized --
+        # the rollout kernels generate each individual's genome from the master
+        # and the GA state, and the GA step runs in the rollout's last workgroup
+        # (one process) or after the all-gather (several ranks)
+        self.fast_step = (not self.torch_rng and self.fused and G <= 4096 and ADV_GENOME <= 4096)
+        self.asked = AskedPopulation(self.state.data_ptr(), self.master.data_ptr(),
+                                     self.master_adv.data_ptr() if arl else None, eng.seed, self.i0, 0)
         # one generation = fixed launches -> replayable HIP graphs: the whole
         # generation on one rank; with several ranks the rollout and the boundary
         # are captured separately around the (eager) all-gather
@@ -342,20 +344,36 @@ class TrainingSession:
                                 self.n_loc, ptr(self.adv_pop), ADV_GENOME, s), "sgmm_ga_ask(adv)")
 
     def _rollout(self):
-        """ask (unless the previous boundary did) + the shard's rollouts
-        (drl_engine.py:104-115, plus the fused validation episodes)."""
+        """ask (host draw / device kernel / generated in-kernel) + the shard's
+        rollouts (drl_engine.py:104-115, plus the fused validation episodes);
+        with one process and the asked population the whole generation,
+        including the GA step, is this one call."""
         P = self.P
+        L, s = self.L, stream_ptr()
+        if self.fast_step:
+            tk, ep = self.ticks.struct(), self.train_eps.struct()
+            ws = self.roll.workspace(self.train_eps, self.arl)
+            f, t = self.out
+            if self.world == 1:
+                check(L.sgmm_generation(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params), ptr(self.state),
+                                        ptr(self.master), ptr(self.master_adv) if self.arl else None,
+                                        ptr(self.best_master), self.H, self.e.seed, P, ptr(f), ptr(t),
+                                        ptr(self.hist), self.generations, ptr(ws), ws.numel(), s),
+                      "sgmm_generation")
+            else:
+                check(L.sgmm_rollout_fitness_asked(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
+                                                   ctypes.byref(self.asked), self.H, ptr(f), ptr(t), ptr(ws),
+                                                   ws.numel(), s), "sgmm_rollout_fitness_asked")
+            return
         if self.torch_rng:
             st_now = self.state.cpu().numpy().view(STATE_DTYPE)[0]
             self.pop.copy_(_host_ask(self.master, float(st_now["sigma_mm"]), P))
             if self.arl:
                 self.adv_pop.copy_(_host_ask(self.master_adv, float(st_now["sigma_adv"]), P))
-        elif not self.fast_step:
+        else:
             self._ask()
         self.roll.fitness(self.ticks, self.train_eps, self.params, self.pop_loc, self.H, self.adv_loc,
                           out=self.out)
-        if self.fused and self.val_eps is not None:
-            self.roll.fitness(self.ticks, self.val_eps, self.params, self.pop_loc, self.H, None, out=self.vout)
 
     def _exchange(self):
         """The generation's one collective: all-gather the per-rank records."""
@@ -363,20 +381,18 @@ class TrainingSession:
             self.rec.all_gather(self.group)
 
     def _boundary(self):
-        """tell both evolvers, validation bookkeeping, sigma decay, next ask."""
+        """tell both evolvers, validation bookkeeping, sigma decay (after the
+        exchange; a no-op when the generation call already did it)."""
         e, L, s = self.e, self.L, stream_ptr()
         P, G = self.P, self.G
         arl = self.arl
         if self.fast_step:
-            # tell + validation + sigma decay in one launch on the gathered
-            # records; the next ask runs as its own many-workgroup kernel (one
-            # workgroup of Philox/Box-Muller is slower than a launch boundary)
-            check(L.sgmm_ga_step(ptr(self.state), *self.rec.step_args(),
-                                 ptr(self.master), ptr(self.master_adv) if arl else None,
-                                 ptr(self.best_master), G, ADV_GENOME if arl else 0, e.seed,
-                                 ptr(self.hist), self.generations, None, None, self.i0, self.n_loc, s),
-                  "sgmm_ga_step")
-            self._ask()
+            if self.world > 1:
+                check(L.sgmm_ga_step(ptr(self.state), *self.rec.step_args(),
+                                     ptr(self.master), ptr(self.master_adv) if arl else None,
+                                     ptr(self.best_master), G, ADV_GENOME if arl else 0, e.seed,
+                                     ptr(self.hist), self.generations, None, None, 0, 0, s),
+                      "sgmm_ga_step")
             return
         tr_f, tr_t, va_f, va_t = self.rec.population()
         # tell both evolvers (model.py:73-76, drl_engine.py:119-125)
@@ -464,7 +480,7 @@ STATE_DTYPE = np.dtype([("sigma_mm", "<f8"), ("sigma_adv", "<f8"), ("best_val", 
                         ("last_train_f", "<f8"), ("last_val_f", "<f8"), ("no_improve", "<i4"),
                         ("best_idx", "<i4"), ("adv_best_idx", "<i4"), ("gen", "<i4"),
                         ("improved", "<i4"), ("decayed", "<i4"), ("patience", "<i4"),
-                        ("pad_", "<i4"), ("decay", "<f8")])
+                        ("arrivals", "<i4"), ("decay", "<f8")])
 assert HIST_DTYPE.itemsize == ctypes_size(GAHistory) and STATE_DTYPE.itemsize == ctypes_size(GAState)
 HIST_STATE_SIZES = (STATE_DTYPE.itemsize, HIST_DTYPE.itemsize)
 

@@ -174,7 +174,7 @@ typedef struct sgmm_ga_state {
     int32_t improved;      /* last generation improved the validation reward */
     int32_t decayed;       /* last generation decayed sigma */
     int32_t patience;      /* 15 (drl_engine.py:155) */
-    int32_t pad_;
+    int32_t arrivals;      /* internal: workgroup arrival counter of fused launches (0 between launches) */
     double  decay;         /* 0.5 (drl_engine.py:156) */
 } sgmm_ga_state;           /* 80 bytes */
 
@@ -241,6 +241,40 @@ int sgmm_ga_step(sgmm_ga_state *state, const double *fitness, const int32_t *tra
                  int64_t n_params_mm, int64_t n_params_adv, uint64_t seed,
                  sgmm_ga_history *history, int32_t history_cap,
                  float *next_pop_mm, float *next_pop_adv, int32_t i0, int32_t n, void *stream);
+
+/* The current generation's ask() population, never materialized: episode e
+ * evaluates individual i0 + genome[e] (adversary: i0 + adv[e], -1 = none)
+ * whose genome is master + sigma * N(0,1) with the state's sigma and
+ * generation -- exactly the rows sgmm_ga_ask would write -- generated inside
+ * the rollout kernels (models/model.py:65-71 fused into drl_engine.py:104-115). */
+typedef struct sgmm_asked_population {
+    const sgmm_ga_state *state;
+    const float *master_mm;   /* [genome_size(hidden)] */
+    const float *master_adv;  /* [1250] or NULL (no adversary) */
+    uint64_t seed;
+    int32_t i0;               /* first individual of this rank's shard */
+    int32_t pad_;
+} sgmm_asked_population;     /* 40 bytes */
+
+/* sgmm_rollout_fitness over the asked population (multi-rank shards: the
+ * results then go through the all-gather and sgmm_ga_step). */
+int sgmm_rollout_fitness_asked(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                               const sgmm_env_params *params, const sgmm_asked_population *pop,
+                               int32_t hidden, double *fitness, int32_t *trades, void *workspace,
+                               size_t workspace_bytes, void *stream);
+
+/* One whole generation of DRLEngine.train on one process
+ * (Env/drl_engine.py:92-171): the asked population's P training episodes
+ * (eps 0..P-1, individual = genome[e]) and P validation episodes (eps
+ * P..2P-1) in one rollout, and the generation boundary of sgmm_ga_step
+ * (tell both evolvers, validation bookkeeping, sigma decay, history row
+ * state->gen) run by the rollout's last workgroup.  fitness/trades: [2P].
+ * Two kernel launches, no host synchronization; genome_size(hidden) <= 4096. */
+int sgmm_generation(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                    const sgmm_env_params *params, sgmm_ga_state *state, float *master_mm,
+                    float *master_adv, float *best_master, int32_t hidden, uint64_t seed,
+                    int32_t P, double *fitness, int32_t *trades, sgmm_ga_history *history,
+                    int32_t history_cap, void *workspace, size_t workspace_bytes, void *stream);
 
 /* Sequential float64 sum init + values[0] + values[1] + ... (device array,
  * result written to *out on the stream): the episode total of

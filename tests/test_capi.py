@@ -44,6 +44,8 @@ def test_struct_layouts_match_header(sgmm):
     assert ctypes.sizeof(_lib.GAHistory) == 40
     assert _lib.Episodes.genome.offset == 24 and ctypes.sizeof(_lib.Episodes) == 72
     assert ctypes.sizeof(_lib.Ticks) == 56
+    assert ctypes.sizeof(_lib.AskedPopulation) == 40 and _lib.AskedPopulation.i0.offset == 32
+    assert _lib.GAState.arrivals.offset == 68
 
 
 def test_argument_errors_need_no_gpu(sgmm):

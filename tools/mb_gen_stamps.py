@@ -1,0 +1,52 @@
+"""Diagnostic: table/scan phase stamps inside the bench generation (asked
+population + fused GA step), stamped library build (tools/build_stamps.sh)."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parent.parent
+os.environ["SGMM_LIB"] = str(ROOT / "tools/mb/libsgmm_stamps.so")
+sys.path.insert(0, str(ROOT))
+import numpy as np
+import torch
+import sgmm_pkg
+sg = sgmm_pkg.load()
+from sgmm_amd import _lib, synthetic
+L = _lib.load()
+L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+P, H, T, Tv = 64, 16, 3600, 720
+tr = synthetic.bundle_510300(T, seed=0)
+va = synthetic.bundle_510300(Tv, seed=1)
+st = synthetic.train_stats(tr)
+torch.manual_seed(0)
+eng = sg.DRLEngine(pop_size=P, phi=1e-4, tick_size=0.001, save_dir="/tmp/mbgen", hidden_dim=H, seed=7,
+                   verbose=False, use_graph=False)
+sess = eng.session(tr, va, st, generations=8)
+for g in range(8):
+    sess.step(g)
+torch.cuda.synchronize()
+nch = (T + 63) // 64
+gx = (nch + 3) // 4
+n_ep = 2 * P
+h = np.zeros((n_ep * gx * 4, 8), np.uint64)
+L.sgmm_debug_tstamps(h.ctypes.data, len(h))
+slots = []
+for e in range(n_ep):
+    Te = T if e < P else Tv
+    for c in range((Te + 63) // 64):
+        slots.append(e * gx * 4 + c)
+h = h[slots].astype(np.int64)
+d = np.diff(h[:, 0:6], axis=1)
+q = lambda a: f"med {np.median(a):.0f} p90 {np.percentile(a, 90):.0f} max {a.max():.0f}"
+print(f"table waves={len(slots)}")
+print(f"  weights     {q(d[:, 0])}\n  mlp         {q(d[:, 1])}\n  env         {q(d[:, 2])}\n"
+      f"  prefix      {q(d[:, 3])}\n  write-drain {q(d[:, 4])}\n  total       {q(h[:, 5] - h[:, 0])}")
+real0 = h[:, 7].min()
+print(f"  wave start ns: {q((h[:, 7] - real0) * 10)}; last end ns {((h[:, 6] - real0) * 10).max():.0f}")
+s = np.zeros((n_ep, 16), np.uint64)
+L.sgmm_debug_stamps(s.ctypes.data, n_ep)
+s = s.astype(np.int64)
+ds = s[:, 1:6] - s[:, [0]]
+print(f"scan (train episodes, median): chunk-starts {np.median(ds[:P,0]):.0f} words {np.median(ds[:P,1]):.0f} "
+      f"gathered {np.median(ds[:P,2]):.0f} summed {np.median(ds[:P,3]):.0f} end {np.median(ds[:P,4]):.0f}")
