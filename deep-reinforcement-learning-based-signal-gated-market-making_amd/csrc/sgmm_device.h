@@ -157,7 +157,10 @@ __device__ __forceinline__ void adv_delta(const float* __restrict__ g, const sgm
 // ---------------------------------------------------------------- cross-lane (DPP)
 // Data-parallel-primitive moves: a VALU operand modifier, no LDS round trip.
 // Lanes whose source is outside the row (or whose row is masked off) get
-// `old`.  GFX9 controls: row_shr:n = 0x110 + n, row_bcast:15 = 0x142,
+// `old`.  Integer / float32 data only: DPP moves fed directly by float64
+// arithmetic measured wrong-but-plausible values on gfx950 (the exact sum
+// stayed exact -- its verification caught every misprediction -- but ran 4x
+// slower), so float64 partial sums are never exchanged this way.  GFX9 controls: row_shr:n = 0x110 + n, row_bcast:15 = 0x142,
 // row_bcast:31 = 0x143.
 template <int CTRL, int ROW_MASK = 0xF>
 __device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
@@ -168,11 +171,6 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
     const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)old, (uint32_t)v);
     const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(old >> 32), (uint32_t)(v >> 32));
     return ((uint64_t)hi << 32) | lo;
-}
-template <int CTRL, int ROW_MASK = 0xF>
-__device__ __forceinline__ double dppf64(double old, double v) {
-    return __longlong_as_double((long long)dpp64<CTRL, ROW_MASK>((uint64_t)__double_as_longlong(old),
-                                                                 (uint64_t)__double_as_longlong(v)));
 }
 // inclusive prefix sums within rows of 16 lanes / over the wave
 __device__ __forceinline__ uint64_t row_scan_add(uint64_t v) {
@@ -186,19 +184,6 @@ __device__ __forceinline__ uint64_t wave_scan_add(uint64_t v) {
     v = row_scan_add(v);
     v += dpp64<0x142, 0xA>(0, v);
     v += dpp64<0x143, 0xC>(0, v);
-    return v;
-}
-__device__ __forceinline__ double row_scan_addf(double v) {
-    v += dppf64<0x111>(0.0, v);
-    v += dppf64<0x112>(0.0, v);
-    v += dppf64<0x114>(0.0, v);
-    v += dppf64<0x118>(0.0, v);
-    return v;
-}
-__device__ __forceinline__ double wave_scan_addf(double v) {
-    v = row_scan_addf(v);
-    v += dppf64<0x142, 0xA>(0.0, v);
-    v += dppf64<0x143, 0xC>(0.0, v);
     return v;
 }
 // inclusive min / max scans within rows of 16 lanes (signed 64-bit)

@@ -573,17 +573,30 @@ struct SumScratch {
 template <int NT>
 __device__ double exact_ordered_sum(const double* sel, int n, double S, SumScratch sc) {
     static_assert(NT % kWave == 0, "whole waves");
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), k = tid & (kSumBlk - 1);
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
     const int nblk = (n + kSumBlk - 1) / kSumBlk;
     const int span = nblk * kSumBlk;
-    // 1a. approximate block sums (any order)
-    constexpr int kIt = (kScanWin + NT - 1) / NT;  // strided passes per thread
+    // Phases 1 and 2 give each thread 4 consecutive ticks: a block of 16
+    // ticks is one quad of lanes (in-register work, 2 DPP steps per scan).
+    // The approximate sums only predict binades (any error just costs a
+    // fallback block), so they run in float32.
+    constexpr int kTpt = 4;
+    constexpr int kIt = (kScanWin + NT * kTpt - 1) / (NT * kTpt);  // passes per thread
+    const int qd = lane & 3;  // position in the quad
+    // 1a. approximate block sums
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
-        const int i = tid + it * NT;
-        if (i < span) {  // uniform per 16-lane row
-            const double v = row_scan_addf(i < n ? sel[i] : 0.0);
-            if (k == kSumBlk - 1) sc.approx[i / kSumBlk] = v;
+        const int i0 = (tid + it * NT) * kTpt;
+        if (i0 < span) {  // uniform per quad
+            double v = 0.0;
+#pragma unroll
+            for (int j = 0; j < kTpt; ++j) v += i0 + j < n ? sel[i0 + j] : 0.0;
+            float f = (float)v;
+            float t = __int_as_float((int)dpp32<0x111>(0u, (uint32_t)__float_as_int(f)));
+            f += qd >= 1 ? t : 0.0f;
+            t = __int_as_float((int)dpp32<0x112>(0u, (uint32_t)__float_as_int(f)));
+            f += qd >= 2 ? t : 0.0f;
+            if (qd == 3) sc.approx[i0 / kSumBlk] = (double)f;
         }
     }
     __syncthreads();
@@ -592,11 +605,18 @@ __device__ double exact_ordered_sum(const double* sel, int n, double S, SumScrat
     if (tid < kWave) {
         double carry = S;
         for (int b0 = 0; b0 < nblk; b0 += kWave) {
-            const int b = b0 + lane;
-            const double v = b < nblk ? sc.approx[b] : 0.0;
-            const double inc = wave_scan_addf(v);
-            if (b < nblk) sc.approx[b] = carry + (inc - v);
-            carry += __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(inc), kWave - 1));
+            const int bb = b0 + lane;
+            const float v = bb < nblk ? (float)sc.approx[bb] : 0.0f;
+            float inc = v;
+            float t;
+#define SGMM_FSTEP(CTRL, RM)                                                                  \
+            t = __int_as_float((int)dpp32<CTRL, RM>(0u, (uint32_t)__float_as_int(inc)));     \
+            inc += t;
+            SGMM_FSTEP(0x111, 0xF) SGMM_FSTEP(0x112, 0xF) SGMM_FSTEP(0x114, 0xF)
+            SGMM_FSTEP(0x118, 0xF) SGMM_FSTEP(0x142, 0xA) SGMM_FSTEP(0x143, 0xC)
+#undef SGMM_FSTEP
+            if (bb < nblk) sc.approx[bb] = carry + (double)(inc - v);
+            carry += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(inc), kWave - 1));
         }
     }
     __syncthreads();
@@ -604,28 +624,55 @@ __device__ double exact_ordered_sum(const double* sel, int n, double S, SumScrat
     // 2. integer steps per block in its predicted binade
 #pragma unroll
     for (int it = 0; it < kIt; ++it) {
-        const int i = tid + it * NT;
-        if (i >= span) continue;  // uniform per 16-lane row
-        const int b = i / kSumBlk;
+        const int i0 = (tid + it * NT) * kTpt;
+        if (i0 >= span) continue;  // uniform per quad
+        const int b = i0 / kSumBlk;
         int e;
         int64_t mdummy;
         const bool fast = binade_of(sc.approx[b], e, mdummy);
-        int64_t d = 0;
+        const double sc52 = pow2(52 - (fast ? e : 0));
         bool bad = !fast;
-        if (fast && i < n) {
-            const double q = sel[i] * pow2(52 - e);
-            bad = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
-            d = bad ? 0 : (int64_t)rint(q);
+        int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+        for (int j = 0; j < kTpt; ++j) {
+            int64_t d = 0;
+            if (fast && i0 + j < n) {
+                const double q = sel[i0 + j] * sc52;
+                const bool bj = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
+                bad |= bj;
+                d = bj ? 0 : (int64_t)rint(q);
+            }
+            P += d;
+            mn = min(mn, P);
+            mx = max(mx, P);
         }
-        const int64_t P = (int64_t)row_scan_add((uint64_t)d);
-        const int64_t mn = row_scan_min(P), mx = row_scan_max(P);
+        // inclusive prefix of the lane totals over the quad
+        uint64_t inc = (uint64_t)P;
+        {
+            uint64_t t = dpp64<0x111>(0, inc);
+            inc += qd >= 1 ? t : 0;
+            t = dpp64<0x112>(0, inc);
+            inc += qd >= 2 ? t : 0;
+        }
+        const int64_t ex = (int64_t)(inc - (uint64_t)P);
+        int64_t qmn = mn + ex, qmx = mx + ex;
+        {
+            int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
+            qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
+            t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
+            qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
+            t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
+            qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
+            t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
+            qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
+        }
         const uint64_t bl = __ballot(bad);
-        if (k == kSumBlk - 1) {
+        if (qd == 3) {
             sc.be[b] = fast ? e : INT32_MIN;
-            sc.pend[b] = P;
-            sc.pmin[b] = mn;
-            sc.pmax[b] = mx;
-            sc.bad[b] = ((bl >> (lane & ~(kSumBlk - 1))) & 0xFFFFu) != 0;
+            sc.pend[b] = (int64_t)inc;
+            sc.pmin[b] = qmn;
+            sc.pmax[b] = qmx;
+            sc.bad[b] = ((bl >> (lane & ~3)) & 0xFu) != 0;
         }
     }
     __syncthreads();

@@ -17,13 +17,15 @@ L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 L.sgmm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 P, H, T, Tv = 64, 16, 3600, 720
 tr = synthetic.bundle_510300(T, seed=0)
-va = synthetic.bundle_510300(Tv, seed=1)
+va = synthetic.bundle_510300(Tv, seed=1, start_ticks=3500)  # bench.py's workload
+SEED = int(sys.argv[1]) if len(sys.argv) > 1 else 99
+GENS = int(sys.argv[2]) if len(sys.argv) > 2 else 8
 st = synthetic.train_stats(tr)
 torch.manual_seed(0)
-eng = sg.DRLEngine(pop_size=P, phi=1e-4, tick_size=0.001, save_dir="/tmp/mbgen", hidden_dim=H, seed=7,
+eng = sg.DRLEngine(pop_size=P, phi=1e-4, tick_size=0.001, save_dir="/tmp/mbgen", hidden_dim=H, seed=SEED,
                    verbose=False, use_graph=False)
-sess = eng.session(tr, va, st, generations=8)
-for g in range(8):
+sess = eng.session(tr, va, st, generations=GENS)
+for g in range(GENS):
     sess.step(g)
 torch.cuda.synchronize()
 nch = (T + 63) // 64
@@ -50,3 +52,9 @@ s = s.astype(np.int64)
 ds = s[:, 1:6] - s[:, [0]]
 print(f"scan (train episodes, median): chunk-starts {np.median(ds[:P,0]):.0f} words {np.median(ds[:P,1]):.0f} "
       f"gathered {np.median(ds[:P,2]):.0f} summed {np.median(ds[:P,3]):.0f} end {np.median(ds[:P,4]):.0f}")
+print(f"scan walk: iterations med {np.median(s[:P,13]):.0f} max {s[:P,13].max()}, slow med {np.median(s[:P,14]):.0f} max {s[:P,14].max()}")
+print(f"scan walk val eps: iterations med {np.median(s[P:,13]):.0f} max {s[P:,13].max()}, slow med {np.median(s[P:,14]):.0f} max {s[P:,14].max()}")
+dd = s[:, 5] - s[:, 0]
+print("scan total cycles per episode: train med", np.median(dd[:P]), "max", dd[:P].max(), "val med", np.median(dd[P:]), "max", dd[P:].max())
+hist = sess.hist[:GENS].cpu().numpy().view(sg.drl_engine.HIST_DTYPE).reshape(-1)
+print("train_f", hist["train_f"], "val_f", hist["val_f"])
