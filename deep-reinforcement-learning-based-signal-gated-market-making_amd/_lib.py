@@ -61,6 +61,18 @@ class AskedPopulation(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("i0", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class DayStreams(ctypes.Structure):
+    _fields_ = [("n_days", ctypes.c_int32), ("pad_", ctypes.c_int32), ("tick_total", ctypes.c_int64)] + \
+        [(n, ctypes.c_void_p) for n in ("snap_off", "snap_time", "bid", "ask", "bidvol", "askvol",
+                                        "tick_off", "tick_time", "price", "volume", "side")]
+
+
+class EventBars(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("n_events", "trade_time", "ask", "bid", "p_buy_max",
+                                               "p_sell_min", "v_buy_sum", "v_sell_sum", "vol_sum",
+                                               "trade_count", "vwap_num")]
+
+
 class GAHistory(ctypes.Structure):
     _fields_ = [("train_f", ctypes.c_double), ("val_f", ctypes.c_double),
                 ("sigma_after", ctypes.c_double), ("train_trades", ctypes.c_int32),
@@ -101,6 +113,12 @@ SIGNATURES = {
                                                   ctypes.c_size_t, _VP]),
     "sgmm_generation": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP, _VP, _VP, _VP, _VP,
                                        _I32, _U64, _I32, _VP, _VP, _VP, _I32, _VP, ctypes.c_size_t, _VP]),
+    "sgmm_event_bars_workspace_size": (ctypes.c_size_t, [_I64]),
+    "sgmm_event_bars_build": (ctypes.c_int, [ctypes.POINTER(DayStreams), ctypes.POINTER(EventBars), _VP,
+                                             ctypes.c_size_t, _VP]),
+    "sgmm_bar_windows": (ctypes.c_int, [ctypes.POINTER(EventBars), _I32, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    "sgmm_step_bundle": (ctypes.c_int, [ctypes.POINTER(EventBars), _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP,
+                                        _VP, _VP, _VP]),
     "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "sgmm_profile_read": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
 }

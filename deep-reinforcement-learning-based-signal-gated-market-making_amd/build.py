@@ -11,8 +11,8 @@ import subprocess
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-SOURCES = ["csrc/sgmm_capi.hip", "csrc/sgmm_rollout.hip", "csrc/sgmm_ga.hip"]
-HEADERS = ["csrc/sgmm_device.h", "csrc/sgmm_internal.h", "../include/sgmm.h"]
+SOURCES = ["csrc/sgmm_capi.hip", "csrc/sgmm_rollout.hip", "csrc/sgmm_ga.hip", "csrc/sgmm_bundle.hip"]
+HEADERS = ["csrc/sgmm_device.h", "csrc/sgmm_internal.h", "csrc/sgmm_ga_device.h", "../include/sgmm.h"]
 ARCH = os.environ.get("SGMM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-Wall",

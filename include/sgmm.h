@@ -282,6 +282,58 @@ int sgmm_generation(const sgmm_ticks *ticks, const sgmm_episodes *eps,
  * bit-identical to the sequential loop.  The rollout uses the same routine. */
 int sgmm_ordered_sum(const double *values, int64_t n, double init, double *out, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Signal-bundle builder: raw snapshot / trade streams
+ * of many trading days -> event bars -> SGU2 input windows -> per-step
+ * bundle.  One workgroup per day.  Columns of day d occupy rows
+ * [off[d], off[d+1]) and must be sorted by trade_time within the day (the
+ * reference sorts with DataFrame.sort_values, HFTLoader.py:29-30).
+ * ------------------------------------------------------------------------ */
+typedef struct sgmm_day_streams {
+    int32_t n_days;
+    int32_t pad_;
+    int64_t tick_total;        /* rows of the trade columns */
+    const int64_t *snap_off;   /* [n_days + 1] */
+    const int64_t *snap_time;  /* HHMMSSmmm */
+    const double *bid, *ask, *bidvol, *askvol;  /* bidprice1 askprice1 bidvol1 askvol1 */
+    const int64_t *tick_off;   /* [n_days + 1] */
+    const int64_t *tick_time;
+    const double *price, *volume;
+    const int32_t *side;       /* +1 buy, -1 sell */
+} sgmm_day_streams;            /* 104 bytes */
+
+/* Event bars of every day, day d's events at rows snap_off[d] .. +n_events[d]
+ * (capacity: the snapshot rows).  Columns as HFTMarketBase.event_df after the
+ * as-of join (HFTLoader.py:26-63); statistics are NaN before the first trade. */
+typedef struct sgmm_event_bars {
+    int32_t *n_events;         /* [n_days] */
+    int64_t *trade_time;
+    double *ask, *bid, *p_buy_max, *p_sell_min, *v_buy_sum, *v_sell_sum, *vol_sum, *trade_count,
+        *vwap_num;
+} sgmm_event_bars;             /* 88 bytes */
+
+size_t sgmm_event_bars_workspace_size(int64_t total_ticks);
+
+/* HFTMarketBase (loaders/HFTLoader.py:26-63) for every day. */
+int sgmm_event_bars_build(const sgmm_day_streams *in, const sgmm_event_bars *out, void *workspace,
+                          size_t workspace_bytes, void *stream);
+
+/* SGU2DataPro.gen_dataset(event_step=19, time_steps=10) (HFTLoader.py:139-169)
+ * for every day: windows of day d at rows win_off[d] .. +n_windows[d] of
+ * X[., 10] / y (float32).  At most 4096 bars (19-event groups) per day. */
+int sgmm_bar_windows(const sgmm_event_bars *ev, int32_t n_days, const int64_t *snap_off,
+                     const int64_t *win_off, float *X, float *y, int32_t *n_windows,
+                     int64_t max_bars_per_day, void *stream);
+
+/* load_signals_bundle's step loop (pipeline/agent_trainer.py:45-78): day d
+ * uses its last n_samples[d] sampled events (every 19th) and writes
+ * n_samples[d]-1 steps at step_off[d]: mid at the next sample, ask/bid at the
+ * sample, buy_max/sell_min over the inclusive .loc window between samples. */
+int sgmm_step_bundle(const sgmm_event_bars *ev, int32_t n_days, const int64_t *snap_off,
+                     const int32_t *n_samples, const int64_t *step_off, int32_t max_steps,
+                     double *mid, double *ask, double *bid, double *buy_max, double *sell_min,
+                     void *stream);
+
 /* Kernel timing for benchmarks / diagnostics (not on by default).
  * While enabled, every kernel the library launches is bracketed by a pair of
  * hipEvents recorded on its stream.  sgmm_profile_read waits for the recorded

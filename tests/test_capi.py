@@ -46,6 +46,8 @@ def test_struct_layouts_match_header(sgmm):
     assert ctypes.sizeof(_lib.Ticks) == 56
     assert ctypes.sizeof(_lib.AskedPopulation) == 40 and _lib.AskedPopulation.i0.offset == 32
     assert _lib.GAState.arrivals.offset == 68
+    assert ctypes.sizeof(_lib.DayStreams) == 104 and _lib.DayStreams.snap_off.offset == 16
+    assert ctypes.sizeof(_lib.EventBars) == 88 and _lib.EventBars.vwap_num.offset == 80
 
 
 def test_argument_errors_need_no_gpu(sgmm):
@@ -58,6 +60,14 @@ def test_argument_errors_need_no_gpu(sgmm):
     assert rc == -1 and b"hidden" in L.sgmm_last_error()
     # no adversary: u32 prefix words + u32 chunk maps + f64 rewards, 256-aligned sections
     assert L.sgmm_rollout_workspace_size(4, 1000, 5) == 4096 + 256 + 40192
+    # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
+    assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
+    rc = L.sgmm_event_bars_build(None, None, None, 0, None)
+    assert rc == -1 and b"null" in L.sgmm_last_error()
+    ev = _lib.EventBars()
+    rc = L.sgmm_bar_windows(ctypes.byref(ev), 1, ctypes.c_void_p(8), ctypes.c_void_p(8), ctypes.c_void_p(8),
+                            ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
+    assert rc == -1 and b"bars per day" in L.sgmm_last_error()
     # adversary (20 states): u64 fill words + f64 rewards
     assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 160000
 
