@@ -117,6 +117,7 @@ SIGNATURES = {
     "sgmm_event_bars_build": (ctypes.c_int, [ctypes.POINTER(DayStreams), ctypes.POINTER(EventBars), _VP,
                                              ctypes.c_size_t, _VP]),
     "sgmm_bar_windows": (ctypes.c_int, [ctypes.POINTER(EventBars), _I32, _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    "sgmm_sgu2_forward": (ctypes.c_int, [_VP, _I32, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),
     "sgmm_step_bundle": (ctypes.c_int, [ctypes.POINTER(EventBars), _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP,
                                         _VP, _VP, _VP]),
     "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),

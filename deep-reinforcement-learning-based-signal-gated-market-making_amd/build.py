@@ -11,7 +11,8 @@ import subprocess
 from pathlib import Path
 
 PKG_DIR = Path(__file__).resolve().parent
-SOURCES = ["csrc/sgmm_capi.hip", "csrc/sgmm_rollout.hip", "csrc/sgmm_ga.hip", "csrc/sgmm_bundle.hip"]
+SOURCES = ["csrc/sgmm_capi.hip", "csrc/sgmm_rollout.hip", "csrc/sgmm_ga.hip", "csrc/sgmm_bundle.hip",
+           "csrc/sgmm_sgu2.hip"]
 HEADERS = ["csrc/sgmm_device.h", "csrc/sgmm_internal.h", "csrc/sgmm_ga_device.h", "../include/sgmm.h"]
 ARCH = os.environ.get("SGMM_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

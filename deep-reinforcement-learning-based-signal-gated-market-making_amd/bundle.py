@@ -106,6 +106,7 @@ class EventBarsGPU:
         nw = nw[:self.n_days].cpu().numpy()
         if (nw < 0).any():
             raise _lib.SgmmError(f"more than 4096 bars on day(s) {np.nonzero(nw < 0)[0].tolist()}")
+        self.X_all, self.win_off, self.n_windows = X, win_off, nw
         return [(X[win_off[d]:win_off[d] + nw[d]].unsqueeze(-1), y[win_off[d]:win_off[d] + nw[d]])
                 for d in range(self.n_days)]
 
@@ -134,12 +135,26 @@ def event_bars(days, device="cuda") -> EventBarsGPU:
     return EventBarsGPU(days, device)
 
 
+def _fused_sgu2(m2, scaler) -> bool:
+    """m2 is this package's SGU2 and the scaler a float32 StandardScaler3D fit
+    (what utils/scaler.py yields for the float32 windows): the transform then
+    is the kernel's float32 (x - mean) / std."""
+    from .gate_units import SGU2
+    mean, std = getattr(scaler, "mean", None), getattr(scaler, "std", None)
+    return (isinstance(m2, SGU2) and type(scaler).__name__ == "StandardScaler3D"
+            and isinstance(mean, np.ndarray) and isinstance(std, np.ndarray)
+            and mean.dtype == np.float32 and std.dtype == np.float32 and mean.size == 1 and std.size == 1)
+
+
 def load_signals_bundle(symbol, date_list, m1, m2, scaler, *, sgu1_features=None, data_root=".",
                         device="cuda"):
     """pipeline/agent_trainer.py:15-78 with the event bars, the SGU2 windows
     and the step loop on the GPU.  ``sgu1_features(event_bars_dict)`` must
     return SGU1DataPro.gen_dataset(19)'s table (with its 'label' column) for
-    one day's event bars."""
+    one day's event bars.  With this package's SGU2 as m2 and a float32
+    StandardScaler3D, SGU2 runs on the device windows of all days at once
+    (gate_units.SGU2.predict_device); any other m2 / scaler gets the host
+    windows as in the reference."""
     import pandas as pd
     if sgu1_features is None:
         raise NotImplementedError("SGU1's feature table (HFTLoader.py:66-135, an xgboost input) is not "
@@ -157,15 +172,21 @@ def load_signals_bundle(symbol, date_list, m1, m2, scaler, *, sgu1_features=None
         kept.append(d)
     ev = EventBarsGPU(days, device)
     wins = ev.windows()
+    s2_all = None
+    if _fused_sgu2(m2, scaler):  # every day's windows through SGU2 in one launch, scaled in the kernel
+        s2_all = m2.predict_device(ev.X_all, scaler).cpu().numpy()
     s1s, s2s, n_samples, used = [], [], [], []
     for k in range(len(days)):
         df1 = sgu1_features(ev.day(k))
-        X2 = wins[k][0].cpu().numpy()
-        if len(df1) == 0 or X2.size == 0:
+        n_win = int(ev.n_windows[k])
+        if len(df1) == 0 or n_win == 0:
             n_samples.append(0)
             continue
         s1 = np.asarray(m1.predict(df1.drop(columns=["label"])))
-        s2 = np.asarray(m2.predict(scaler.transform(X2))).flatten()
+        if s2_all is not None:
+            s2 = s2_all[ev.win_off[k]:ev.win_off[k] + n_win]
+        else:
+            s2 = np.asarray(m2.predict(scaler.transform(wins[k][0].cpu().numpy()))).flatten()
         n = min(len(s1), len(s2))
         s1s.append(s1[-n:][:-1])
         s2s.append(s2[-n:][:-1])

@@ -334,6 +334,23 @@ int sgmm_step_bundle(const sgmm_event_bars *ev, int32_t n_days, const int64_t *s
                      double *mid, double *ask, double *bid, double *buy_max, double *sell_min,
                      void *stream);
 
+/* ------------------------------------------------------------------------
+ * SGU2 inference
+ * ------------------------------------------------------------------------ */
+
+/* SGU2.predict (models/GateUnits.py:116-120): SGU2Model.forward in eval mode
+ * (GateUnits.py:42-54 -- nn.LSTM(1, hidden) over each window, last hidden
+ * state, Linear(hidden, 1)) for n windows X[n, time_steps, 1] (float32, the
+ * windows of sgmm_bar_windows).  weights: float32 in state_dict order --
+ * lstm.weight_ih_l0[4H,1], lstm.weight_hh_l0[4H,H], lstm.bias_ih_l0[4H],
+ * lstm.bias_hh_l0[4H], fc.weight[1,H], fc.bias[1].  mean/std: the float32
+ * StandardScaler3D fit (utils/scaler.py:9-18; agent_trainer.py:43 scales
+ * before predict), applied in the kernel, or both NULL for unscaled input.
+ * out: float32[n].  hidden in {10, 16, 32}. */
+int sgmm_sgu2_forward(const float *weights, int32_t hidden, const float *X, int64_t n,
+                      int32_t time_steps, const float *mean, const float *std, float *out,
+                      void *stream);
+
 /* Kernel timing for benchmarks / diagnostics (not on by default).
  * While enabled, every kernel the library launches is bracketed by a pair of
  * hipEvents recorded on its stream.  sgmm_profile_read waits for the recorded
