@@ -19,6 +19,10 @@ SCRIPT = textwrap.dedent(r"""
     assert FTPEnv is sgmm_amd.FTPEnv and DRLEngine is sgmm_amd.DRLEngine
     assert TradingPolicy is sgmm_amd.TradingPolicy
     assert evaluate_individual is sgmm_amd.evaluate_individual
+    from models.GateUnits import SGU1, SGU2
+    from utils.scaler import StandardScaler3D
+    import sgmm_amd.gate_units as gu
+    assert SGU2 is gu.SGU2 and StandardScaler3D is gu.StandardScaler3D
 
     d = dict(np.load({golden!r}, allow_pickle=False))
     st = dict(zip(("s1_m", "s1_s", "s2_m", "s2_s"), d["stats"]))
