@@ -50,6 +50,7 @@ struct EpArrays {
     const int32_t* len;
     const int64_t* step_off;
     const int32_t* param;
+    int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -201,11 +202,12 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
         const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
         const double mid = spx[0][lane], ask = spx[1][lane], bid = spx[2][lane];
         const double bmax = spx[3][lane], smin = spx[4][lane];
-        double* __restrict__ R = rew + (ep.step_off[e] + t0 + lane) * ns;
+        const int64_t row = ep.step_off[e] + t0 + lane;
+        double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
         if (!ARL) {
             const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
             code[w][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
-            R[w] = so.reward;
+            rew[w * ep.rs + row] = so.reward;
         } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -458,7 +460,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     uint64_t fw = 0;
     if (valid) {
         const double mid = tmid, ask = task, bid = tbid, bmax = tbmax, smin = tsmin;
-        double* __restrict__ R = rew + row * ns;
+        double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
         map = 0;
 #pragma unroll
         for (int si = 0; si < NSI; ++si) {
@@ -470,7 +472,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
                 const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
                 map |= (uint32_t)(si + so.fill_buy - so.fill_sell) << (3 * si);
                 traded |= (uint32_t)(so.fill_buy | so.fill_sell) << si;
-                R[si] = so.reward;
+                rew[si * ep.rs + row] = so.reward;
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -871,7 +873,6 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
         }
     }
     SGMM_STAMP(e, 1);
-    const int ns = nsi;
     int my_trades = 0;
     double total = 0.0;
     for (int w0 = 0; w0 < T; w0 += kScanWin) {
@@ -889,7 +890,7 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
                 if (i < n) {
                     wdv[p] = wl[i];
                     stv[p] = map_get(wdv[p], start[(w0 + i) / kChunk]);
-                    r[p] = rew[(so + w0 + i) * ns + stv[p]];
+                    r[p] = rew[stv[p] * ep.rs + so + w0 + i];
                 }
             }
 #pragma unroll
@@ -919,6 +920,346 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
         trades_out[e] = tr;
     }
     if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
+}
+
+// ------------------------------------------------------------------ exact ordered sum v2
+// The same exact sum as exact_ordered_sum, restructured around latency for a
+// 1024-thread workgroup whose threads hold the values in registers: thread
+// tid owns elements 4 tid .. 4 tid + 3 of a 4096-element window, so a 16-element
+// summation block is one quad of lanes.
+//   1. approximate block starts: a float32 wave scan + the waves' totals
+//      (one barrier);
+//   2. each block's predicted binade, its integer steps, their quad prefix
+//      range, the tie / huge flags, and the block sums' wave-level exclusive
+//      prefix -> per-block records in LDS (one barrier);
+//   3. wave 0 holds the records of blocks 64 j + lane in registers (4 per lane)
+//      and walks: each iteration is one masked range check per register slot
+//      and a scalar find-first; a failing block is added the reference way
+//      from the window's values in LDS (one barrier, S broadcast).
+// Every accepted shortcut is exact (see exact_ordered_sum), so the result is
+// the sequential float64 sum bit for bit.
+constexpr int kTpt2 = 4;                          // elements per thread
+constexpr int kWin2 = kScanThreads * kTpt2;       // elements per window
+constexpr int kBlk2 = kWin2 / kSumBlk;            // 16-element blocks per window
+constexpr int kWaves2 = kScanThreads / kWave;     // waves per workgroup
+constexpr int kSlots2 = kBlk2 / kWave;            // walk: blocks per lane
+static_assert(kSumBlk == 4 * kTpt2, "a block is one quad of lanes");
+static_assert(kSlots2 == 4, "pick4");
+
+// inclusive float32 prefix sum over the wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ float wave_scan_add_f32(float v) {
+#define SGMM_FSTEP2(CTRL, RM) \
+    v += __int_as_float((int)dpp32<CTRL, RM>(0u, (uint32_t)__float_as_int(v)));
+    SGMM_FSTEP2(0x111, 0xF) SGMM_FSTEP2(0x112, 0xF) SGMM_FSTEP2(0x114, 0xF)
+    SGMM_FSTEP2(0x118, 0xF) SGMM_FSTEP2(0x142, 0xA) SGMM_FSTEP2(0x143, 0xC)
+#undef SGMM_FSTEP2
+    return v;
+}
+
+template <typename V>
+__device__ __forceinline__ V pick4(const V (&a)[kSlots2], int j) {  // j wave-uniform
+    return j == 0 ? a[0] : j == 1 ? a[1] : j == 2 ? a[2] : a[3];
+}
+
+struct SumLds2 {
+    double sel[kWin2];  // the window's values (fallback blocks)
+    int32_t be[kBlk2];  // predicted binade (INT32_MIN: none / tie / huge step)
+    int64_t mn[kBlk2], mx[kBlk2];  // range of the block's inclusive integer prefixes
+    uint64_t z[kBlk2];  // wave-local exclusive prefix of the block sums
+    float w_ap[kWaves2];
+    uint64_t w_z[kWaves2];
+    double S;
+};
+
+// All kScanThreads threads call after L.sel[0, n) holds the window's values
+// and a barrier; returns S + sel[0] + ... + sel[n-1] in sequential float64
+// order in every thread.  S must be identical in every thread.  Ends with a
+// barrier (L.sel may then be refilled).
+__device__ __forceinline__ double exact_sum_window(int n, double S, SumLds2& L) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6, qd = lane & 3;
+    const int i0 = tid * kTpt2;
+    double r[kTpt2];
+#pragma unroll
+    for (int j = 0; j < kTpt2; ++j) r[j] = i0 + j < n ? L.sel[i0 + j] : 0.0;
+    // 1. approximate block starts (only binade predictions: float32 is enough)
+    const float fv = (float)(((r[0] + r[1]) + r[2]) + r[3]);
+    const float finc = wave_scan_add_f32(fv);
+    const float fbs = __int_as_float((int)dpp32<0x00>(0u, (uint32_t)__float_as_int(finc - fv)));
+    if (lane == kWave - 1) L.w_ap[wv] = finc;
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 8);
+    float woff = 0.0f;  // the preceding waves' totals (broadcast reads, in order)
+#pragma unroll
+    for (int k = 0; k < kWaves2; ++k) woff += k < wv ? L.w_ap[k] : 0.0f;
+    // 2. integer steps of the block in its predicted binade
+    int eb;
+    int64_t mdummy;
+    const bool fast = binade_of(S + (double)(woff + fbs), eb, mdummy);
+    const double sc52 = pow2(52 - (fast ? eb : 0));
+    bool bad = !fast;
+    int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+    for (int j = 0; j < kTpt2; ++j) {
+        int64_t d = 0;
+        if (fast && i0 + j < n) {
+            const double q = r[j] * sc52;
+            const bool bj = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
+            bad |= bj;
+            d = bj ? 0 : (int64_t)rint(q);
+        }
+        P += d;
+        mn = min(mn, P);
+        mx = max(mx, P);
+    }
+    uint64_t qinc = (uint64_t)P;  // inclusive prefix of the lane totals over the quad
+    {
+        uint64_t t = dpp64<0x111>(0, qinc);
+        qinc += qd >= 1 ? t : 0;
+        t = dpp64<0x112>(0, qinc);
+        qinc += qd >= 2 ? t : 0;
+    }
+    const int64_t ex = (int64_t)(qinc - (uint64_t)P);
+    int64_t qmn = mn + ex, qmx = mx + ex;
+    {
+        int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
+        qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
+        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
+        qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
+        t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
+        qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
+        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
+        qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
+    }
+    const uint64_t bl = __ballot(bad);
+    const uint64_t bt = qd == 3 ? qinc : 0;  // block total at the quad's last lane
+    const uint64_t zinc = wave_scan_add(bt);
+    if (lane == kWave - 1) L.w_z[wv] = zinc;
+    if (qd == 3) {
+        const int b = wv * (kWave / 4) + (lane >> 2);
+        L.be[b] = (fast && ((bl >> (lane & ~3)) & 0xFu) == 0) ? eb : INT32_MIN;
+        L.mn[b] = qmn;
+        L.mx[b] = qmx;
+        L.z[b] = zinc - bt;
+    }
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 9);
+    // 3. the walk (wave 0; every lane carries the same S)
+    if (wv == 0) {
+        const uint64_t wz = lane < kWaves2 ? L.w_z[lane] : 0;
+        const uint64_t wzi = wave_scan_add(wz);
+        const uint64_t zend = readlane64(wzi, kWave - 1);
+        const uint64_t wzx = wzi - wz;  // exclusive prefix of the wave totals
+        const int nblk = (n + kSumBlk - 1) / kSumBlk;
+        int ber[kSlots2];
+        int64_t mnr[kSlots2], mxr[kSlots2];
+        uint64_t zr[kSlots2];
+#pragma unroll
+        for (int j = 0; j < kSlots2; ++j) {
+            const int b = kWave * j + lane;
+            const int src = b / (kWave / 4);  // the wave that produced block b
+            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)wzx, src, kWave);
+            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(wzx >> 32), src, kWave);
+            ber[j] = L.be[b];
+            mnr[j] = L.mn[b];
+            mxr[j] = L.mx[b];
+            zr[j] = L.z[b] + (((uint64_t)hi << 32) | lo);
+        }
+        SGMM_STAMP(blockIdx.x, 10);
+#ifdef SGMM_STAMPS
+        unsigned long long n_iter = 0, n_slow = 0, c_fast = 0, c_slow = 0, t_a, t_b, t_c;
+#endif
+        int pos = 0;
+        while (pos < nblk) {
+#ifdef SGMM_STAMPS
+            ++n_iter;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_a) : "v"(S) : "memory");
+#endif
+            S = uniform_f64(S);  // wave-uniform: scalar control flow below
+            int f = pos, eS;
+            int64_t M;
+            if (binade_of(S, eS, M)) {
+                // M at the start of block b if blocks pos .. b-1 are all accepted: K + z[b]
+                const uint64_t K = (uint64_t)M - readlane64(pick4(zr, pos / kWave), pos % kWave);
+                f = nblk;
+#pragma unroll
+                for (int j = 0; j < kSlots2; ++j) {
+                    if (f == nblk && kWave * j < nblk && kWave * (j + 1) > pos) {
+                        const int b = kWave * j + lane;
+                        const uint64_t c = K + zr[j];
+                        const int64_t lo = (int64_t)(c + (uint64_t)mnr[j]);
+                        const int64_t hi = (int64_t)(c + (uint64_t)mxr[j]);
+                        const bool inr = M > 0 ? (lo >= kMLo && hi <= kMHi) : (hi <= -kMLo && lo >= -kMHi);
+                        const bool ok = b < pos || b >= nblk || (ber[j] == eS && inr);
+                        const uint64_t fails = __ballot(!ok);
+                        if (fails) f = kWave * j + __ffsll((unsigned long long)fails) - 1;
+                    }
+                }
+                if (f > pos) {
+                    const uint64_t zf = f < nblk ? readlane64(pick4(zr, f / kWave), f % kWave) : zend;
+                    S = from_binade((int64_t)(K + zf), eS);
+                }
+            }
+#ifdef SGMM_STAMPS
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_b) : "v"(S), "s"(f) : "memory");
+            c_fast += t_b - t_a;
+#endif
+            if (f < nblk) {  // this block the reference way
+#ifdef SGMM_STAMPS
+                ++n_slow;
+#endif
+                const int t0 = f * kSumBlk, m = min(kSumBlk, n - t0);
+                double v[kSumBlk];
+#pragma unroll
+                for (int j = 0; j < kSumBlk; ++j) v[j] = L.sel[t0 + min(j, m - 1)];
+                if (m == kSumBlk) {
+#pragma unroll
+                    for (int j = 0; j < kSumBlk; ++j) S += v[j];
+                } else {  // the window's last block
+#pragma unroll
+                    for (int j = 0; j < kSumBlk; ++j)
+                        if (j < m) S += v[j];
+                }
+                pos = f + 1;
+#ifdef SGMM_STAMPS
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_c) : "v"(S) : "memory");
+                c_slow += t_c - t_b;
+#endif
+            } else {
+                pos = nblk;
+            }
+        }
+        SGMM_STAMP(blockIdx.x, 11);
+#ifdef SGMM_STAMPS
+        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; g_stamps[blockIdx.x][15] = c_fast; g_stamps[blockIdx.x][7] = c_slow; }
+#endif
+        if (lane == 0) L.S = S;
+    }
+    __syncthreads();
+    return L.S;
+}
+
+// ------------------------------------------------------------------ path scan v2 (no adversary)
+// The same result as k_path_scan_maps, restructured around latency: one
+// workgroup (16 waves) per episode, 4096-tick windows.
+//   0. loads issued at entry, before anything waits: wave 0's chunk maps, then
+//      every thread's prefix words and all ns rewards (SoA rows) of ticks
+//      tid + 1024 p -- each load instruction reads 512 contiguous bytes;
+//   1. wave 0: chunk start states -> LDS                             [barrier]
+//   2. per tick: state, selected reward (register select) -> LDS, traded bit
+//                                                                    [barrier]
+//   3. exact_sum_window on the selected rewards         [3 barriers per window]
+template <int NSM>
+__global__ __launch_bounds__(kScanThreads) void k_path_scan_v2(
+    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
+    const uint32_t* __restrict__ words, const uint32_t* __restrict__ cmaps,
+    const double* __restrict__ rew, double* __restrict__ fitness,
+    int32_t* __restrict__ trades_out, StepArgs step) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    SumLds2& L = *reinterpret_cast<SumLds2*>(lds);
+    __shared__ uint8_t start[kMaxLen / kChunk];
+    __shared__ int red_trades;
+    const int e = blockIdx.x;
+    const int32_t T = ep.len[e];
+    const int nch = (T + kChunk - 1) / kChunk;
+    const int64_t so = ep.step_off[e];
+    const uint32_t cb = chunk_base(so, e);
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
+    const int ns = nsi;
+    if (tid == 0) red_trades = 0;
+
+    // ---- 0. loads: wave 0's first chunk maps, then every thread's window-0 data
+    const uint32_t cm0 = (wv == 0 && lane < nch) ? cmaps[cb + lane] : kIdentityMap;
+    uint32_t wd[kTpt2];
+    double rv[kTpt2][NSM];
+#define SGMM_LOAD_WINDOW(W0, N)                                                    \
+    _Pragma("unroll") for (int p = 0; p < kTpt2; ++p) {                            \
+        const int i = p * kScanThreads + tid;                                      \
+        wd[p] = 0;                                                                 \
+        if (i < (N)) {                                                             \
+            wd[p] = words[so + (W0) + i];                                          \
+            _Pragma("unroll") for (int s = 0; s < NSM; ++s)                        \
+                rv[p][s] = s < ns ? rew[s * ep.rs + so + (W0) + i] : 0.0;          \
+        }                                                                          \
+    }
+    SGMM_STAMP(e, 0);
+    SGMM_LOAD_WINDOW(0, min(kWin2, T))
+    // ---- 1. chunk start states (wave 0), 64 chunks per round
+    if (wv == 0) {
+        uint32_t s = (uint32_t)(-inv_min);
+        for (int c0 = 0; c0 < nch; c0 += kWave) {
+            const int c = c0 + lane;
+            const uint32_t m = c0 == 0 ? cm0 : (c < nch ? cmaps[cb + c] : kIdentityMap);
+            uint32_t inc = m;
+#pragma unroll
+            for (int d = 1; d < kWave; d <<= 1) {
+                const uint32_t before = __shfl_up(inc, d, kWave);
+                if (lane >= d) inc = map_then<NSM>(before, inc);
+            }
+            uint32_t excl = __shfl_up(inc, 1, kWave);
+            if (lane == 0) excl = kIdentityMap;
+            if (c < nch) start[c] = (uint8_t)map_get(excl, s);
+            s = map_get(__shfl(inc, kWave - 1, kWave), s);
+        }
+    }
+    SGMM_STAMP(e, 1);
+    __syncthreads();
+    SGMM_STAMP(e, 2);
+
+    int my_trades = 0;
+    double S = 0.0;  // exact running sum (identical in every thread between windows)
+    for (int w0 = 0; w0 < T; w0 += kWin2) {
+        const int n = min(kWin2, T - w0);
+        if (w0 > 0) {
+            SGMM_LOAD_WINDOW(w0, n)
+        }
+        // ---- 2. states and selected rewards (a wave's 64 ticks are one chunk)
+#pragma unroll
+        for (int p = 0; p < kTpt2; ++p) {
+            const int i = p * kScanThreads + tid;
+            if (i < n) {
+                const uint32_t st = map_get(wd[p], start[(w0 + i) / kChunk]);
+                double x = rv[p][0];
+#pragma unroll
+                for (int s = 1; s < NSM; ++s) x = st == (uint32_t)s ? rv[p][s] : x;
+                L.sel[i] = x;
+                my_trades += (wd[p] >> (24 + st)) & 1u;
+            }
+        }
+        __syncthreads();
+        SGMM_STAMP(e, 3);
+        // ---- 3. the window's exact sum
+        S = exact_sum_window(n, S, L);
+        SGMM_STAMP(e, 4);
+    }
+#undef SGMM_LOAD_WINDOW
+    int wsum = my_trades;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
+    if (lane == 0 && wsum) atomicAdd(&red_trades, wsum);
+    __syncthreads();
+    if (tid == 0) {
+        const int tr = red_trades;
+        double total = S;
+        if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
+        fitness[e] = total;
+        trades_out[e] = tr;
+    }
+    SGMM_STAMP(e, 5);
+    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
+}
+
+// ordered sum through exact_sum_window (sgmm_ordered_sum's default kernel)
+__global__ __launch_bounds__(kScanThreads) void k_ordered_sum_v2(const double* __restrict__ x, int64_t n,
+                                                                 double init, double* __restrict__ out) {
+    __shared__ SumLds2 L;
+    double S = init;
+    for (int64_t w0 = 0; w0 < n; w0 += kWin2) {
+        const int m = (int)min((int64_t)kWin2, n - w0);
+        for (int i = threadIdx.x; i < m; i += kScanThreads) L.sel[i] = x[w0 + i];
+        __syncthreads();
+        S = exact_sum_window(m, S, L);
+    }
+    if (threadIdx.x == 0) *out = S;
 }
 
 // ------------------------------------------------------------------ ordered sum (standalone)
@@ -1215,9 +1556,11 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     return SGMM_OK;
 }
 
+static int64_t rew_stride(int64_t steps) { return (steps + 31) & ~int64_t(31); }
+
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param};
+                    e->param, rew_stride(e->total_steps)};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -1228,6 +1571,14 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 static int table_path() {
     const char* e = std::getenv("SGMM_TABLE_PATH");
     return (e && std::strcmp(e, "valu") == 0) ? 1 : 0;
+}
+
+// Path-scan kernel selection: 1 = the windowed k_path_scan_maps (default),
+// 0 = k_path_scan_v2 (SGMM_SCAN=v2; A/B measurements and a cross-check in the
+// tests -- it loads all ns rewards per tick up front, which measured slower).
+static int scan_path() {
+    const char* e = std::getenv("SGMM_SCAN");
+    return (e && std::strcmp(e, "v2") == 0) ? 0 : 1;
 }
 
 }  // namespace sgmm
@@ -1246,7 +1597,8 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
 //   u32 words[total_steps] | u32 cmaps[total_steps/64 + n + 1] (no adversary)
 //   u64 fills[total_steps]                                  (adversary)
-//   f64 rew[total_steps * n_states]
+//   f64 rew: no adversary [n_states][rs] (rs = total_steps rounded up to 32),
+//            adversary [total_steps][n_states]
 static size_t ws_words(int64_t steps) { return align256((size_t)steps * sizeof(uint32_t)); }
 static size_t ws_cmaps(int32_t n, int64_t steps) {
     return align256(((size_t)steps / kChunk + (size_t)n + 1) * sizeof(uint32_t));
@@ -1258,7 +1610,9 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
     if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
     const size_t head = n_states > 8 ? ws_fills(total_steps)
                                      : ws_words(total_steps) + ws_cmaps(n_episodes, total_steps);
-    return head + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
+    if (n_states > 8)  // adversary: rew[row * n_states + state]
+        return head + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
+    return head + (size_t)rew_stride(total_steps) * (size_t)n_states * sizeof(double);
 }
 
 template <int H>
@@ -1302,8 +1656,12 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
     clear_error();
     SGMM_REQUIRE(out && (values || n == 0) && n >= 0, "bad arguments");
     ProfScope prof("ordered_sum", as_stream(stream));
-    hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
-                       init, out);
+    if (scan_path() == 0)
+        hipLaunchKernelGGL(k_ordered_sum_v2, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values,
+                           n, init, out);
+    else
+        hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
+                           init, out);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }
@@ -1366,6 +1724,18 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         hipLaunchKernelGGL(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
+        if (scan_path() == 0) {
+            size_t lds = sizeof(SumLds2);
+            if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
+            if (nsi <= 5)
+                hipLaunchKernelGGL(k_path_scan_v2<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
+                                   params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
+            else
+                hipLaunchKernelGGL(k_path_scan_v2<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
+                                   params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
+            SGMM_LAUNCHED();
+            return SGMM_OK;
+        }
         size_t lds = kScanWin * (sizeof(double) + sizeof(uint32_t)) + nch_max;
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
         if (nsi <= 5)

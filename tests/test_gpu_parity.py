@@ -237,6 +237,21 @@ def test_dropin_evaluate_individual(golden, sgmm):
         assert f == ep["fitness"] and t == ep["trades"]
 
 
+@pytest.mark.parametrize("scan", ["v2", "v1"])
+def test_scan_paths_agree(golden, sgmm, oracle, scan, monkeypatch):
+    """Both path-scan kernels reproduce the oracle on the fixtures and on ragged
+    lengths around the chunk / block / window boundaries."""
+    monkeypatch.setenv("SGMM_SCAN", scan)
+    eps = [e for e in episodes_from_fixture(golden("g2_synthetic.npz")) if e["adv"] is None]
+    lens = [0, 1, 15, 16, 17, 63, 64, 65, 4095, 4096, 4097, 8193, 12000]
+    eps += _synthetic_batch(sgmm, len(lens), max(lens), 16, seed=13, lengths=lens, sigma=0.3)
+    for (H, arl), group in _groups(eps).items():
+        (fit, trd), _ = _run_batch(sgmm, group, arl)
+        for i, ep in enumerate(group):
+            f, t = _oracle_eval(oracle, ep)
+            assert trd[i].item() == t and fit[i].item() == f, (scan, H, i)
+
+
 @pytest.mark.parametrize("path", ["valu", "mfma"])
 def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
     """The f32-MFMA and the VALU table kernels both reproduce the oracle's
@@ -280,9 +295,12 @@ def _sum_cases():
             ("n16", 0.0, env_like[:16]), ("n17", 0.0, env_like[:17]), ("n4097", 0.0, env_like[:4097] * 1e3)]
 
 
+@pytest.mark.parametrize("scan", ["v2", "v1"])
 @pytest.mark.parametrize("name,init,x", _sum_cases(), ids=[c[0] for c in _sum_cases()])
-def test_ordered_sum_matches_sequential(sgmm, name, init, x):
-    """The parallel exact episode sum equals total += r in float64, bit for bit."""
+def test_ordered_sum_matches_sequential(sgmm, name, init, x, scan, monkeypatch):
+    """The parallel exact episode sum equals total += r in float64, bit for bit
+    (v2: exact_sum_window, the path scan's sum; v1: exact_ordered_sum)."""
+    monkeypatch.setenv("SGMM_SCAN", scan)
     from sgmm_amd import _lib
     L = _lib.load()
     xd = torch.from_numpy(np.ascontiguousarray(x, np.float64)).to(DEV)
