@@ -158,14 +158,13 @@ def main():
                          val_mode="fused", sync_every=10**9, verbose=False,
                          use_graph=not args.no_graph)
     sess = eng.session(train, val, stats, generations=args.warmup + args.steps)
-    for g in range(args.warmup):
-        sess.step(g)
+    sess.steps(0, args.warmup)
+    sess.capture()  # graphs recorded (not run) before the timed region
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for g in range(args.warmup, args.warmup + args.steps):
-        sess.step(g)
+    sess.steps(args.warmup, args.steps)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

@@ -200,10 +200,11 @@ class DRLEngine:
 
     def train(self, train_bundle, val_bundle, train_stats, generations=100, output_prefix="agent"):
         sess = self.session(train_bundle, val_bundle, train_stats, generations, output_prefix)
-        for gen in range(generations):
-            sess.step(gen)
-            if (gen + 1) % self.sync_every == 0:
-                sess.flush(gen + 1)
+        for gen in range(0, generations, self.sync_every):
+            n = min(self.sync_every, generations - gen)
+            sess.steps(gen, n)
+            if n == self.sync_every:
+                sess.flush(gen + n)
         return sess.finish()
 
 
@@ -298,6 +299,7 @@ class TrainingSession:
         # are captured separately around the (eager) all-gather
         self.use_graph = bool(eng.use_graph) and not self.torch_rng
         self.graphs = None
+        self.graph_batch = max(1, min(self.GRAPH_BATCH, eng.sync_every))
         self.roll.reserve(self.train_eps, arl)
         if self.val_eps is not None:
             self.roll.reserve(self.val_eps, False)
@@ -320,6 +322,20 @@ class TrainingSession:
             self._exchange()
             self._boundary()
             return
+        self.capture()
+        self.graphs[0].replay()
+        if self.world > 1:
+            self._exchange()
+            self.graphs[1].replay()
+
+    # generations per captured multi-generation graph (one process)
+    GRAPH_BATCH = 16
+
+    def capture(self):
+        """Record (without running) the generation graphs: one generation, and
+        with one process a batch of min(GRAPH_BATCH, sync_every) generations."""
+        if not self.use_graph:
+            return
         if self.graphs is None:
             self.graphs = []
             phases = [(self._rollout, self._boundary)] if self.world == 1 else [(self._rollout,), (self._boundary,)]
@@ -329,10 +345,34 @@ class TrainingSession:
                     for f in fns:
                         f()
                 self.graphs.append(g)
-        self.graphs[0].replay()
-        if self.world > 1:
-            self._exchange()
-            self.graphs[1].replay()
+        if self.world == 1 and self.graph_batch > 1 and getattr(self, "batch_graph", None) is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.graph_batch):
+                    self._rollout()
+                    self._boundary()
+            self.batch_graph = g
+
+    def steps(self, gen0: int, n: int):
+        """Enqueue generations gen0 .. gen0 + n - 1 (same as n step() calls).
+
+        With one process and use_graph, whole batches of GRAPH_BATCH
+        generations are captured once in a single HIP graph and replayed: one
+        host launch per batch instead of per generation (the host-side graph
+        launch, not the GPU, set the pace of single-generation replays)."""
+        if not self.use_graph or self.world > 1:
+            for g in range(gen0, gen0 + n):
+                self.step(g)
+            return
+        B = self.graph_batch
+        done = 0
+        if B > 1 and n >= B:
+            self.capture()
+            while n - done >= B:
+                self.batch_graph.replay()
+                done += B
+        for g in range(gen0 + done, gen0 + n):
+            self.step(g)
 
     def _ask(self):
         """ask() of the shard (models/model.py:65-71) from the device master/sigma."""
