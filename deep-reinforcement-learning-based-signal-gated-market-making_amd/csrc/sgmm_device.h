@@ -266,11 +266,11 @@ __device__ __forceinline__ void ask_row4(const float* __restrict__ master, int64
 
 // first index of the maximum, NaN counting as the maximum (np.argmax)
 __device__ __forceinline__ bool better(double a, int ia, double b, int ib) {
+    // branch-free (selects, no divergent control flow inside shuffle reductions)
     const bool na = a != a, nb = b != b;
-    if (na != nb) return na;
-    if (na) return ia < ib;
-    if (a != b) return a > b;
-    return ia < ib;
+    const bool tie = na || a == b;
+    const bool ord = tie ? (ia < ib) : (a > b);
+    return na == nb ? ord : na;
 }
 
 // Population results gathered shard by shard: individual i's value lives in

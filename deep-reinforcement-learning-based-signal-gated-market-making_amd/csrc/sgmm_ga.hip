@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
     __shared__ int si[2 * kStepBlock];
     __shared__ float lm[kMaxStepParams];
     __shared__ float la[kMaxStepParams];
-    ga_step_dev(st, fit, trades, vfit, vtrades, P, shard, master, master_adv, best_master, n_mm,
+    ga_step_dev<false>(st, fit, trades, vfit, vtrades, P, shard, master, master_adv, best_master, n_mm,
                 n_adv, seed, history, hist_cap, next_mm, next_adv, i0, n, sv, si, lm, la);
 }
 

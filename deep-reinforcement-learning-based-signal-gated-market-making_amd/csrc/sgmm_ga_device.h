@@ -13,33 +13,98 @@ namespace sgmm {
 // ---------------------------------------------------------------- fused boundary
 constexpr int kStepBlock = 1024;
 
+// Loads of the fitness records.  HANDOFF: they were stored in this launch by
+// other workgroups with write-through (sc1) stores, so every load of them is a
+// global sc1 load (MI355X_MICROARCH.md, inter-workgroup visibility, row 1:
+// one storing lane per workgroup, agent-scope arrival ticket, the last
+// arriver loads) -- no acquire fence, no L2 invalidate.
+template <bool HANDOFF, class T>
+__device__ __forceinline__ T ld_rec(const T* p) {
+    if constexpr (HANDOFF) {
+        typedef __attribute__((address_space(1))) const T gT;
+        return __hip_atomic_load((gT*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        return *p;
+    }
+}
+
+template <bool HANDOFF, class T>
+__device__ __forceinline__ T shard_ld(const T* __restrict__ base, ShardView v, int i) {
+    if (v.n <= 0) return ld_rec<HANDOFF>(base + i);
+    const char* q = reinterpret_cast<const char*>(base) + (int64_t)(i / v.n) * v.stride;
+    return ld_rec<HANDOFF>(reinterpret_cast<const T*>(q) + i % v.n);
+}
+
+__device__ __forceinline__ void argmax_merge(double& bv, int& bi, double ov, int oi) {
+    const bool take = oi >= 0 && (bi < 0 || better(ov, oi, bv, bi));
+    bv = take ? ov : bv;
+    bi = take ? oi : bi;
+}
+
+// np.argmax over one wave (first index on ties, NaN first), lanes with
+// valid: a NaN ballot, a max butterfly, a ballot of the lanes equal to the
+// max.  Returns the winning lane (-1: no valid lane) and its value.
+__device__ __forceinline__ int wave_argmax_first(double f, bool valid, double& bv) {
+    const uint64_t nan = __ballot(valid && f != f);
+    if (nan) {  // wave-uniform
+        bv = __longlong_as_double(0x7FF8000000000000LL);
+        return __ffsll((unsigned long long)nan) - 1;
+    }
+    double m = valid ? f : -__builtin_inf();
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, kWave));
+    const uint64_t hit = __ballot(valid && f == m);
+    bv = m;
+    return hit ? __ffsll((unsigned long long)hit) - 1 : -1;
+}
+
+// np.argmax of fit and of -fit (first index on ties, NaN first) over the
+// workgroup: strided scan, wave shuffles, one LDS round over the waves.
+// LDS scratch: sv[2*nt] doubles, si[2*nt] ints.
+template <bool HANDOFF>
 __device__ void block_argmax2(const double* __restrict__ fit, ShardView sv_, int P, int& best,
                               int& abest, double* sv, int* si) {
-    const int tid = threadIdx.x, nt = blockDim.x;
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int nw = (nt + kWave - 1) / kWave;
     double bv = 0.0, av = 0.0;
     int bi = -1, aj = -1;
     for (int i = tid; i < P; i += nt) {
-        const double f = shard_at(fit, sv_, i);
-        if (bi < 0 || better(f, i, bv, bi)) { bv = f; bi = i; }
-        if (aj < 0 || better(-f, i, av, aj)) { av = -f; aj = i; }
+        const double f = shard_ld<HANDOFF>(fit, sv_, i);
+        argmax_merge(bv, bi, f, i);
+        argmax_merge(av, aj, -f, i);
     }
-    sv[tid] = bv; si[tid] = bi;
-    sv[nt + tid] = av; si[nt + tid] = aj;
-    __syncthreads();
-    for (int w = nt / 2; w > 0; w >>= 1) {
-        if (tid < w) {
 #pragma unroll
-            for (int r = 0; r < 2; ++r) {
-                const int o = r * nt;
-                const int io = si[o + tid + w];
-                if (io >= 0 && (si[o + tid] < 0 || better(sv[o + tid + w], io, sv[o + tid], si[o + tid]))) {
-                    sv[o + tid] = sv[o + tid + w];
-                    si[o + tid] = io;
-                }
-            }
-        }
-        __syncthreads();
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        const double ob = __shfl_down(bv, off, kWave), oa = __shfl_down(av, off, kWave);
+        const int oib = __shfl_down(bi, off, kWave), oia = __shfl_down(aj, off, kWave);
+        argmax_merge(bv, bi, ob, oib);
+        argmax_merge(av, aj, oa, oia);
     }
+    if (lane == 0) {
+        sv[wv] = bv;
+        si[wv] = bi;
+        sv[nt + wv] = av;
+        si[nt + wv] = aj;
+    }
+    __syncthreads();
+    if (wv == 0) {
+        bv = lane < nw ? sv[lane] : 0.0;
+        bi = lane < nw ? si[lane] : -1;
+        av = lane < nw ? sv[nt + lane] : 0.0;
+        aj = lane < nw ? si[nt + lane] : -1;
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) {
+            const double ob = __shfl_down(bv, off, kWave), oa = __shfl_down(av, off, kWave);
+            const int oib = __shfl_down(bi, off, kWave), oia = __shfl_down(aj, off, kWave);
+            argmax_merge(bv, bi, ob, oib);
+            argmax_merge(av, aj, oa, oia);
+        }
+        if (lane == 0) {
+            si[0] = bi;
+            si[nt] = aj;
+        }
+    }
+    __syncthreads();
     best = si[0];
     abest = si[nt];
 }
@@ -76,6 +141,9 @@ __device__ void ask_rows(const float* lds_master, int64_t n, float sig, uint64_t
 // size): tell both evolvers, validation bookkeeping, sigma decay, history
 // row, and optionally the next generation's ask of [i0, i0+n).
 // LDS scratch: sv[2*nt] doubles, si[2*nt] ints, lm[n_mm], la[n_adv] floats.
+// HANDOFF: the fitness records come from other workgroups of this launch
+// (sc1 loads, see ld_rec).
+template <bool HANDOFF>
 __device__ void ga_step_dev(sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
                             const int32_t* __restrict__ trades, const double* __restrict__ vfit,
                             const int32_t* __restrict__ vtrades, int32_t P, ShardView shard,
@@ -88,46 +156,57 @@ __device__ void ga_step_dev(sgmm_ga_state* __restrict__ st, const double* __rest
     const uint32_t gen = (uint32_t)st->gen;
     sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
     int best, abest;
-    block_argmax2(fit, shard, P, best, abest, sv, si);
+    block_argmax2<HANDOFF>(fit, shard, P, best, abest, sv, si);
     const float sig_mm = (float)st->sigma_mm, sig_adv = (float)st->sigma_adv;
     __syncthreads();  // sv/si are reused below
     // tell (model.py:73-76; drl_engine.py:119-125)
     regen_master(master, lm, n_mm, sig_mm, seed, 0u, gen, best);
     if (master_adv) regen_master(master_adv, la, n_adv, sig_adv, seed, 1u, gen, abest);
     if (tid == 0) {
-        // validation of the best (drl_engine.py:129-171)
-        const double v = shard_at(vfit, shard, best);
-        const int improved = v > st->best_val;
+        // validation of the best (drl_engine.py:129-171); every load issued
+        // before the first dependent use
+        const double v = shard_ld<HANDOFF>(vfit, shard, best);
+        const double tf = shard_ld<HANDOFF>(fit, shard, best);
+        const int32_t ttr = trades ? shard_ld<HANDOFF>(trades, shard, best) : 0;
+        const int32_t vtr = vtrades ? shard_ld<HANDOFF>(vtrades, shard, best) : 0;
+        const double best_val = st->best_val, decay = st->decay;
+        double smm = st->sigma_mm, sadv = st->sigma_adv;
+        int32_t no_improve = st->no_improve;
+        const int32_t patience = st->patience;
+        const int improved = v > best_val;
         int decayed = 0;
         if (improved) {
             st->best_val = v;
-            st->no_improve = 0;
+            no_improve = 0;
         } else {
-            st->no_improve += 1;
+            no_improve += 1;
         }
-        if (st->no_improve >= st->patience) {
-            st->sigma_mm *= st->decay;
-            st->sigma_adv *= st->decay;
-            st->no_improve = 0;
+        if (no_improve >= patience) {
+            smm *= decay;
+            sadv *= decay;
+            no_improve = 0;
             decayed = 1;
         }
+        st->sigma_mm = smm;
+        st->sigma_adv = sadv;
+        st->no_improve = no_improve;
         st->best_idx = best;
         st->adv_best_idx = abest;
-        st->last_train_f = shard_at(fit, shard, best);
+        st->last_train_f = tf;
         st->improved = improved;
         st->decayed = decayed;
         st->last_val_f = v;
-        st->gen += 1;
+        st->gen = (int32_t)gen + 1;
         si[0] = improved;
-        sv[0] = st->sigma_mm;
-        sv[1] = st->sigma_adv;
+        sv[0] = smm;
+        sv[1] = sadv;
         if (hist) {
-            hist->train_f = shard_at(fit, shard, best);
-            hist->train_trades = trades ? shard_at(trades, shard, best) : 0;
+            hist->train_f = tf;
+            hist->train_trades = ttr;
             hist->best_idx = best;
             hist->val_f = v;
-            hist->val_trades = vtrades ? shard_at(vtrades, shard, best) : 0;
-            hist->sigma_after = st->sigma_mm;
+            hist->val_trades = vtr;
+            hist->sigma_after = smm;
             hist->flags = improved | (decayed << 1);
         }
     }
@@ -139,6 +218,195 @@ __device__ void ga_step_dev(sgmm_ga_state* __restrict__ st, const double* __rest
     // ask of the next generation (model.py:65-71) from the new master / sigma
     if (next_mm) ask_rows(lm, n_mm, next_sig_mm, seed, 0u, gen + 1, i0, n, next_mm);
     if (next_adv && master_adv) ask_rows(la, n_adv, next_sig_adv, seed, 1u, gen + 1, i0, n, next_adv);
+}
+
+// The fused generation tail's GA step (sgmm_generation: one workgroup, the
+// records contiguous, P <= blockDim.x).  The same results as ga_step_dev, laid
+// out for latency: every record (sc1) and the masters are loaded up front, the
+// argmax carries the best individual's validation record through its
+// shuffles, and the masters are regenerated from registers.
+constexpr int kTailSlots = 4;  // float4 master chunks per thread (n <= 16 * blockDim.x)
+
+#ifdef SGMM_STAMPS
+static __device__ unsigned long long g_tail[8];  // diagnostic build: tail phase times (thread 0)
+#define SGMM_TAIL_STAMP(k, dep)                                                      \
+    do {                                                                             \
+        unsigned long long t_;                                                       \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" \
+                     : "=s"(t_) : "v"(dep) : "memory");                              \
+        if (threadIdx.x == 0) g_tail[k] = t_;                                        \
+    } while (0)
+#else
+#define SGMM_TAIL_STAMP(k, dep) \
+    do {                        \
+    } while (0)
+#endif
+
+__device__ __forceinline__ void argmax_merge_p(double& bv, int& bi, double& pv, int& pt, int& pvt,
+                                               double ov, int oi, double opv, int opt, int opvt) {
+    const bool take = oi >= 0 && (bi < 0 || better(ov, oi, bv, bi));
+    bv = take ? ov : bv;
+    bi = take ? oi : bi;
+    pv = take ? opv : pv;
+    pt = take ? opt : pt;
+    pvt = take ? opvt : pvt;
+}
+
+__device__ __forceinline__ void load_master4(const float* __restrict__ m, int64_t n,
+                                             float (&r)[kTailSlots][4]) {
+#pragma unroll
+    for (int j = 0; j < kTailSlots; ++j) {
+        const int64_t k4 = threadIdx.x + (int64_t)j * blockDim.x;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[j][q] = 4 * k4 + q < n ? m[4 * k4 + q] : 0.0f;
+    }
+}
+
+__device__ __forceinline__ void regen_master_regs(float* __restrict__ master, float* lds_master,
+                                                  int64_t n, const float (&m)[kTailSlots][4],
+                                                  float sig, uint64_t seed, uint32_t sid,
+                                                  uint32_t gen, int best) {
+#pragma unroll
+    for (int j = 0; j < kTailSlots; ++j) {
+        const int64_t k4 = threadIdx.x + (int64_t)j * blockDim.x;
+        if (4 * k4 >= n) break;
+        float z[4];
+        normal4(seed, sid, gen, (uint32_t)best, (uint32_t)k4, z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * k4 + q < n) {
+                const float v = m[j][q] + z[q] * sig;  // ask_row4's arithmetic
+                master[4 * k4 + q] = v;
+                lds_master[4 * k4 + q] = v;
+            }
+    }
+}
+
+template <bool HANDOFF>
+__device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
+                              const int32_t* __restrict__ trades, const double* __restrict__ vfit,
+                              const int32_t* __restrict__ vtrades, int32_t P,
+                              float* __restrict__ master, float* __restrict__ master_adv,
+                              float* __restrict__ best_master, int64_t n_mm, int64_t n_adv,
+                              uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap,
+                              double* sv, int* si, float* lm, float* la) {
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int nw = (nt + kWave - 1) / kWave;
+    // ---- every load first
+    double f = 0.0, vf = 0.0;
+    int tr = 0, vtr = 0;
+    const bool mine = tid < P;
+    if (mine) {
+        f = ld_rec<HANDOFF>(fit + tid);
+        vf = ld_rec<HANDOFF>(vfit + tid);
+        if (trades) tr = ld_rec<HANDOFF>(trades + tid);
+        if (vtrades) vtr = ld_rec<HANDOFF>(vtrades + tid);
+    }
+    float mm[kTailSlots][4], ma[kTailSlots][4];
+    load_master4(master, n_mm, mm);
+    if (master_adv) load_master4(master_adv, n_adv, ma);
+    const int32_t gen_i = st->gen;
+    const uint32_t gen = (uint32_t)gen_i;
+    const double st_smm = st->sigma_mm, st_sadv = st->sigma_adv, best_val = st->best_val,
+                 decay = st->decay;
+    const int32_t no_improve0 = st->no_improve, patience = st->patience;
+    const float sig_mm = (float)st_smm, sig_adv = (float)st_sadv;
+    SGMM_TAIL_STAMP(0, f + vf + mm[0][0] + sig_mm);
+    // ---- argmax of fit (payload: the validation record) and of -fit: the
+    // waves holding records reduce with shuffles, every thread merges their
+    // results from LDS
+    const int nwa = (P + kWave - 1) / kWave;
+    double bv = f, pv = vf, av = -f;
+    int bi = mine ? tid : -1, pt = tr, pvt = vtr, aj = bi;
+    if (wv < nwa) {
+        const int bl = wave_argmax_first(f, mine, bv);
+        const int al = wave_argmax_first(-f, mine, av);
+        const int src = bl < 0 ? 0 : bl;
+        pv = __shfl(vf, src, kWave);
+        pt = __shfl(tr, src, kWave);
+        pvt = __shfl(vtr, src, kWave);
+        bi = bl < 0 ? -1 : wv * kWave + bl;
+        aj = al < 0 ? -1 : wv * kWave + al;
+        // per-wave results: sv[0..nw) best, sv[nw..2nw) its validation fitness, sv[2nw..3nw)
+        // adversary; si[0..nw) best idx, si[nw..2nw) trades, si[2nw..3nw) val trades,
+        // si[3nw..4nw) adversary idx
+        if (lane == 0) {
+            sv[wv] = bv;
+            sv[nw + wv] = pv;
+            sv[2 * nw + wv] = av;
+            si[wv] = bi;
+            si[nw + wv] = pt;
+            si[2 * nw + wv] = pvt;
+            si[3 * nw + wv] = aj;
+        }
+    }
+    SGMM_TAIL_STAMP(6, bv);
+    __syncthreads();
+    SGMM_TAIL_STAMP(7, bv);
+    bv = sv[0];
+    pv = sv[nw];
+    av = sv[2 * nw];
+    bi = si[0];
+    pt = si[nw];
+    pvt = si[2 * nw];
+    aj = si[3 * nw];
+    for (int w = 1; w < nwa; ++w) {
+        argmax_merge_p(bv, bi, pv, pt, pvt, sv[w], si[w], sv[nw + w], si[nw + w], si[2 * nw + w]);
+        argmax_merge(av, aj, sv[2 * nw + w], si[3 * nw + w]);
+    }
+    const int best = bi, abest = aj;
+    SGMM_TAIL_STAMP(1, best + abest);
+    // ---- tell (model.py:73-76; drl_engine.py:119-125)
+    regen_master_regs(master, lm, n_mm, mm, sig_mm, seed, 0u, gen, best);
+    if (master_adv) regen_master_regs(master_adv, la, n_adv, ma, sig_adv, seed, 1u, gen, abest);
+    SGMM_TAIL_STAMP(2, lm[0]);
+    __syncthreads();  // every wave has read sv/si; lm/la complete
+    SGMM_TAIL_STAMP(3, lm[0]);
+    if (tid == 0) {  // validation of the best (drl_engine.py:129-171)
+        const double v = pv, tf = bv;
+        double smm = st_smm, sadv = st_sadv;
+        int32_t no_improve = no_improve0;
+        const int improved = v > best_val;
+        int decayed = 0;
+        if (improved) {
+            st->best_val = v;
+            no_improve = 0;
+        } else {
+            no_improve += 1;
+        }
+        if (no_improve >= patience) {
+            smm *= decay;
+            sadv *= decay;
+            no_improve = 0;
+            decayed = 1;
+        }
+        st->sigma_mm = smm;
+        st->sigma_adv = sadv;
+        st->no_improve = no_improve;
+        st->best_idx = best;
+        st->adv_best_idx = abest;
+        st->last_train_f = tf;
+        st->improved = improved;
+        st->decayed = decayed;
+        st->last_val_f = v;
+        st->gen = gen_i + 1;
+        if (history && gen_i < hist_cap) {
+            sgmm_ga_history* hist = history + gen_i;
+            hist->train_f = tf;
+            hist->train_trades = pt;
+            hist->best_idx = best;
+            hist->val_f = v;
+            hist->val_trades = pvt;
+            hist->sigma_after = smm;
+            hist->flags = improved | (decayed << 1);
+        }
+        si[0] = improved;
+    }
+    SGMM_TAIL_STAMP(4, si[0]);
+    __syncthreads();
+    if (si[0] && best_master)
+        for (int64_t k = tid; k < n_mm; k += nt) best_master[k] = lm[k];
+    SGMM_TAIL_STAMP(5, si[0]);
 }
 
 }  // namespace sgmm

@@ -138,15 +138,18 @@ __device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
 // SGPR operands, each used once (no loop-invariant hoisting, no SGPR spills,
 // ~H+16 VGPRs -> full occupancy).  The 64-tick slice of the tick stream is
 // staged once in LDS (coalesced) and read by all waves.  Wave 0 then turns the
-// per-state fills into the chunk's transition maps.  Outputs per tick:
-//   !ARL: words[row] = exclusive prefix map of the tick within its 64-tick
-//         chunk | traded-mask << 24; cmaps[chunk] = the chunk's full map;
-//    ARL: fills[row] = 2 fill bits per (inventory, sell flag, buy flag) state;
-// and rew[row * ns + state] = the step reward from that state (float64).
+// per-state fills into the chunk's transition maps.  Outputs:
+//   !ARL: per chunk, cmaps[chunk] = the chunk's full transition map and
+//         ctr[chunk] = the trade count along the chunk's path from each start
+//         state (8 bits per state); per tick, the path planes
+//         rew[s * rs + row] = the reward of the tick along the chunk's path
+//         that starts in state s (float64);
+//    ARL: fills[row] = 2 fill bits per (inventory, sell flag, buy flag) state
+//         and rew[row * ns + state] = the step reward from that state.
 template <int H, int NSM, bool ARL>
 __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
-    GenomeSrc src, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
     uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
@@ -164,6 +167,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     __shared__ float sx[2][kChunk];
     __shared__ double spx[5][kChunk];
     __shared__ uint8_t code[32][kChunk];
+    __shared__ double rws[ARL ? 1 : NSM][kChunk];  // !ARL: per-state rewards for the path planes
     __shared__ int32_t lut[2][32];
     // stage the tick slice: column c by wave c % nsi
     const int64_t tbase = ep.tick_off[e] + t0;
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
         if (!ARL) {
             const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
             code[w][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
-            rew[w * ep.rs + row] = so.reward;
+            rws[ARL ? 0 : w][lane] = so.reward;
         } else {
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -248,8 +252,17 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     }
     uint32_t excl = __shfl_up(inc, 1, kWave);
     if (lane == 0) excl = kIdentityMap;
-    if (valid) words[row] = (excl & 0x00FFFFFFu) | (traded << 24);
-    if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + blockIdx.x] = inc;
+    uint64_t cnt = 0;
+    for (int s0 = 0; s0 < nsi; ++s0) {
+        const uint32_t st = map_get(excl, (uint32_t)s0);
+        if (valid) rew[s0 * ep.rs + row] = rws[ARL ? 0 : st][lane];
+        cnt |= (uint64_t)__popcll(__ballot(valid && ((traded >> st) & 1u))) << (8 * s0);
+    }
+    if (lane == kWave - 1) {
+        const uint32_t ci = chunk_base(ep.step_off[e], e) + blockIdx.x;
+        cmaps[ci] = inc;
+        ctr[ci] = cnt;
+    }
 }
 
 #ifdef SGMM_STAMPS
@@ -314,7 +327,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <int H, int NSI, bool ARL>
 __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfma(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
-    GenomeSrc src, int32_t inv_min, int32_t nsi, uint32_t* __restrict__ words,
+    GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
     uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     static_assert(H % 16 == 0, "MFMA table needs H multiple of 16");
     using L = GenomeLayout<H>;
@@ -458,6 +471,12 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     }
     uint32_t map = kIdentityMap, traded = 0;
     uint64_t fw = 0;
+    // [state][lane] rewards, staged in the activation buffer (the MLP is done
+    // with it; the asm is a compiler memory barrier: float and double views of
+    // the same LDS must not be reordered)
+    double* rl = reinterpret_cast<double*>(hb);
+    static_assert(NSI * 2 <= HP, "reward staging fits the activation buffer");
+    asm volatile("" ::: "memory");
     if (valid) {
         const double mid = tmid, ask = task, bid = tbid, bmax = tbmax, smin = tsmin;
         double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
@@ -472,7 +491,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
                 const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
                 map |= (uint32_t)(si + so.fill_buy - so.fill_sell) << (3 * si);
                 traded |= (uint32_t)(so.fill_buy | so.fill_sell) << si;
-                rew[si * ep.rs + row] = so.reward;
+                rl[si * kWave + lane] = so.reward;
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
@@ -499,8 +518,23 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     uint32_t excl = __shfl_up(inc, 1, kWave);
     if (lane == 0) excl = kIdentityMap;
     SGMM_TSTAMP(wslot, 4, excl);
-    if (valid) words[row] = (excl & 0x00FFFFFFu) | (traded << 24);
-    if (lane == kWave - 1) cmaps[chunk_base(ep.step_off[e], e) + chunk] = inc;
+    // path planes: plane s holds the reward along the chunk's path from start
+    // state s; per start state the path's trade count (8 bits each)
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int s0 = 0; s0 < NSI; ++s0) {
+        if (s0 >= nsi) break;
+        const uint32_t st = map_get(excl, (uint32_t)s0);
+        if (valid) rew[s0 * ep.rs + row] = rl[st * kWave + lane];
+        cnt |= (uint64_t)__popcll(__ballot(valid && ((traded >> st) & 1u))) << (8 * s0);
+    }
+    if (lane == kWave - 1) {
+        const uint32_t ci = chunk_base(ep.step_off[e], e) + chunk;
+        cmaps[ci] = inc;
+        ctr[ci] = cnt;
+    }
 #ifdef SGMM_STAMPS
     SGMM_TSTAMP(wslot, 5, 0);
     SGMM_TSTAMP_REAL(wslot, 6);
@@ -515,22 +549,32 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
 // multiple M of u = 2^(e-52), and fl(S + r) = (M + rint(r/u)) * u exactly as
 // long as the exact S + r stays inside the binade and r/u is not a tie (x.5).
 // So a stretch of ticks that keeps one binade adds up as 64-bit integers.
-//   1. blocks of 16 ticks: approximate sums (any order) -> approximate start
-//      of every block -> predicted binade of every block;
-//   2. per block and predicted binade: integer steps d = rint(r/u), their
-//      16-lane prefix (end, min, max) and a flag for ties / huge steps;
-//   3. one wave walks the blocks from the exact S: a run of blocks whose
-//      predicted binade is S's and whose prefix range keeps M strictly inside
-//      [2^52, 2^53) is added in one integer prefix; the first block that fails
-//      (binade change, tie, zero/subnormal S, NaN) is added sequentially in
-//      float64 -- the reference operation -- and the walk resumes after it.
+//
+// A window of 4 NT values (NT threads, 4 consecutive values each, a 16-value
+// block = one quad of lanes):
+//   a. float32 approximate block starts (wave scan + the waves' totals);
+//   b. per block: the binade predicted from its approximate start, its integer
+//      steps d = rint(r/u), their prefix range and a flag for ties / huge
+//      steps.  Blocks of one wave that share a predicted binade form a run;
+//      every block gets the record of the rest of its run (segmented suffix
+//      min / max of the integer prefixes, the run's integer sum, its end);
+//   c. one wave walks the blocks from the exact S with scalar control flow:
+//      if S's binade is the block's prediction and M plus the run's prefix
+//      range stays strictly inside [2^52, 2^53), the whole rest of the run is
+//      added as one integer; otherwise the block is added with the reference's
+//      float64 additions (its values are already in registers) and the walk
+//      moves to the next block.
 // Every accepted shortcut is exact by the property above, so the result is
-// the sequential sum bit for bit.
+// the sequential sum bit for bit.  On a bench episode the walk takes ~10
+// fallback blocks (the sum's doublings: ticks 2, 3, 6, 16, 22, 43, 85, ...)
+// and a few run jumps per 256-value wave.
 constexpr int kSumBlk = 16;
-constexpr int kScanThreads = 1024;
-constexpr int kScanWin = 4096;  // ticks resident per window (32 KB of rewards)
-constexpr int kScanBlks = kScanWin / kSumBlk;
+constexpr int kSumTpt = 4;          // values per thread
+constexpr int kScanThreads = 1024;  // path-scan workgroup
+constexpr int kScanWin = kScanThreads * kSumTpt;
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
+constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
+static_assert(kSumBlk == 4 * kSumTpt, "a block is one quad of lanes");
 
 // S = M * 2^(e-52) with |M| in [2^52, 2^53); false unless S is normal with
 // |e| <= 900 (the shortcut's range: 2^(52-e) and its inverse stay normal)
@@ -556,218 +600,248 @@ __device__ __forceinline__ double uniform_f64(double v) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+__device__ __forceinline__ int64_t uniform_i64(int64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ double pow2(int k) {  // k in [-1022, 1023]
     return __longlong_as_double((int64_t)(k + 1023) << 52);
 }
 
-struct SumScratch {
-    double* approx;   // [nblk] approximate block sums, then block starts
-    int32_t* be;      // [nblk] predicted binade (INT32_MIN: none)
-    int64_t* pend;    // [nblk] integer step sum of the block
-    int64_t* pmin;    // [nblk] min / max of its inclusive prefixes
-    int64_t* pmax;
-    uint64_t* z;      // [nblk] exclusive prefix of pend (mod 2^64; meaningful across same-binade runs)
-    uint8_t* bad;     // [nblk] tie / huge step / no binade
+__device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
+    const int lo = __shfl((int)(uint32_t)v, src, kWave);
+    const int hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src, kWave);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// inclusive float32 prefix sum over the wave (DPP row shifts + row broadcasts)
+__device__ __forceinline__ float wave_scan_add_f32(float v) {
+#define SGMM_FSTEP(CTRL, RM) \
+    v += __int_as_float((int)dpp32<CTRL, RM>(0u, (uint32_t)__float_as_int(v)));
+    SGMM_FSTEP(0x111, 0xF) SGMM_FSTEP(0x112, 0xF) SGMM_FSTEP(0x114, 0xF)
+    SGMM_FSTEP(0x118, 0xF) SGMM_FSTEP(0x142, 0xA) SGMM_FSTEP(0x143, 0xC)
+#undef SGMM_FSTEP
+    return v;
+}
+
+// the walk's view of block b: the rest of its run [b, rend)
+struct SumRec {
+    int64_t mn, mx;  // min / max of the integer prefixes over the run, relative to b's start
+    int64_t dsum;    // integer sum of blocks b .. rend-1
+    int32_t be;      // predicted binade (INT32_MIN: none, tie, huge step, or past the end)
+    int32_t rend;    // first block after b (window index) with another prediction, or the wave's end
 };
 
-// All NT threads call; returns the exact sequential sum S + sel[0] + ... +
-// sel[n-1] in wave 0 (other waves: unspecified).  Ends with a barrier.
 template <int NT>
-__device__ double exact_ordered_sum(const double* sel, int n, double S, SumScratch sc) {
-    static_assert(NT % kWave == 0, "whole waves");
-    const int tid = threadIdx.x, lane = tid & (kWave - 1);
-    const int nblk = (n + kSumBlk - 1) / kSumBlk;
-    const int span = nblk * kSumBlk;
-    // Phases 1 and 2 give each thread 4 consecutive ticks: a block of 16
-    // ticks is one quad of lanes (in-register work, 2 DPP steps per scan).
-    // The approximate sums only predict binades (any error just costs a
-    // fallback block), so they run in float32.
-    constexpr int kTpt = 4;
-    constexpr int kIt = (kScanWin + NT * kTpt - 1) / (NT * kTpt);  // passes per thread
-    const int qd = lane & 3;  // position in the quad
-    // 1a. approximate block sums
+struct SumLds {
+    SumRec rec[NT / 4];
+    float w_ap[NT / kWave];
+    double S;
+};
+
+// All NT threads call once sel[0, n) holds the window's values (n <= 4 NT)
+// and a barrier has passed; returns S + sel[0] + ... + sel[n-1] in sequential
+// float64 order in every thread.  S must be the same in every thread.  Ends
+// with a barrier (sel may then be refilled).
+template <int NT>
+__device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L) {
+    static_assert(NT % kWave == 0 && NT / 4 <= (1 << 30), "whole waves");
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6, qd = lane & 3, q = lane >> 2;
+    const int i0 = tid * kSumTpt;
+    double r[kSumTpt];
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const int i0 = (tid + it * NT) * kTpt;
-        if (i0 < span) {  // uniform per quad
-            double v = 0.0;
+    for (int j = 0; j < kSumTpt; ++j) r[j] = i0 + j < n ? sel[i0 + j] : 0.0;
+    // the last block padded with -0.0 (x + -0.0 == x for every x, -0.0 and NaN
+    // included), so a fallback block always adds 16 values
+    if (i0 < ((n + kSumBlk - 1) & ~(kSumBlk - 1)))
 #pragma unroll
-            for (int j = 0; j < kTpt; ++j) v += i0 + j < n ? sel[i0 + j] : 0.0;
-            float f = (float)v;
-            float t = __int_as_float((int)dpp32<0x111>(0u, (uint32_t)__float_as_int(f)));
-            f += qd >= 1 ? t : 0.0f;
-            t = __int_as_float((int)dpp32<0x112>(0u, (uint32_t)__float_as_int(f)));
-            f += qd >= 2 ? t : 0.0f;
-            if (qd == 3) sc.approx[i0 / kSumBlk] = (double)f;
-        }
-    }
+        for (int j = 0; j < kSumTpt; ++j)
+            if (i0 + j >= n) const_cast<double*>(sel)[i0 + j] = -0.0;
+    // a. approximate block starts (binade predictions only: float32 is enough)
+    const float fv = (float)(((r[0] + r[1]) + r[2]) + r[3]);
+    const float finc = wave_scan_add_f32(fv);
+    const float fbs = __int_as_float((int)dpp32<0x00>(0u, (uint32_t)__float_as_int(finc - fv)));
+    if (lane == kWave - 1) L.w_ap[wv] = finc;
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 8);
-    // 1b. approximate block starts (wave 0)
-    if (tid < kWave) {
-        double carry = S;
-        for (int b0 = 0; b0 < nblk; b0 += kWave) {
-            const int bb = b0 + lane;
-            const float v = bb < nblk ? (float)sc.approx[bb] : 0.0f;
-            float inc = v;
-            float t;
-#define SGMM_FSTEP(CTRL, RM)                                                                  \
-            t = __int_as_float((int)dpp32<CTRL, RM>(0u, (uint32_t)__float_as_int(inc)));     \
-            inc += t;
-            SGMM_FSTEP(0x111, 0xF) SGMM_FSTEP(0x112, 0xF) SGMM_FSTEP(0x114, 0xF)
-            SGMM_FSTEP(0x118, 0xF) SGMM_FSTEP(0x142, 0xA) SGMM_FSTEP(0x143, 0xC)
-#undef SGMM_FSTEP
-            if (bb < nblk) sc.approx[bb] = carry + (double)(inc - v);
-            carry += (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(inc), kWave - 1));
+    float woff = 0.0f;  // the preceding waves' totals (broadcast reads, in order)
+#pragma unroll
+    for (int k = 0; k < NT / kWave; ++k) woff += k < wv ? L.w_ap[k] : 0.0f;
+    // b. integer steps of the block in its predicted binade
+    const bool blive = (tid & ~3) * kSumTpt < n;  // the block has values (uniform per quad)
+    int eb = 0;
+    int64_t ma = 0;  // the approximate start's mantissa
+    const bool fast = blive && binade_of(S + (double)(woff + fbs), eb, ma);
+    const double sc52 = pow2(52 - (fast ? eb : 0));
+    bool bad = !fast;
+    int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
+#pragma unroll
+    for (int j = 0; j < kSumTpt; ++j) {
+        int64_t d = 0;
+        if (fast && i0 + j < n) {
+            const double qv = r[j] * sc52;
+            const bool bj = !(fabs(qv) < 0x1p56) || (qv - floor(qv) == 0.5);
+            bad |= bj;
+            d = bj ? 0 : (int64_t)rint(qv);
         }
+        P += d;
+        mn = min(mn, P);
+        mx = max(mx, P);
+    }
+    // inclusive prefix of the lane totals over the quad (the DPP moves run in
+    // every lane: a move whose source lane is inactive returns 0)
+    uint64_t qinc = (uint64_t)P;
+    {
+        const uint64_t t1 = dpp64<0x111>(0, qinc);
+        qinc += qd >= 1 ? t1 : 0;
+        const uint64_t t2 = dpp64<0x112>(0, qinc);
+        qinc += qd >= 2 ? t2 : 0;
+    }
+    const int64_t ex = (int64_t)(qinc - (uint64_t)P);
+    int64_t qmn = mn + ex, qmx = mx + ex;
+    {
+        int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
+        qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
+        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
+        qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
+        t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
+        qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
+        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
+        qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
+    }
+    // a block whose predicted prefix comes within 2^-12 of the binade's edges
+    // (the float32 start's error is far below that) most likely crosses it:
+    // no prediction, so the runs before it stay fast and it is added the
+    // reference way
+    const bool edge = qd == 3 && fast &&
+                      (ma > 0 ? (ma + qmx > kMHi - kEdge || ma + qmn < kMLo + kEdge)
+                              : (ma + qmn < -kMHi + kEdge || ma + qmx > -kMLo - kEdge));
+    const uint64_t bl = __ballot(bad || edge);
+    const int32_t be = (fast && ((bl >> (lane & ~3)) & 0xFu) == 0) ? eb : INT32_MIN;
+    // block sums at the quad leaders (qd == 3) -> wave-local exclusive prefix zl
+    const uint64_t bt = qd == 3 ? qinc : 0;
+    const uint64_t zinc = wave_scan_add(bt);
+    const int64_t zl = (int64_t)(zinc - bt);
+    const int64_t wtot = (int64_t)readlane64(zinc, kWave - 1);
+    // runs inside the wave: a leader starts a run when its prediction differs
+    // from the previous block's
+    const int32_t bprev = __shfl_up(be, 4, kWave);
+    const uint64_t starts = __ballot(qd == 3 && (q == 0 || be != bprev));
+    const uint64_t later = lane == kWave - 1 ? 0ull : starts & (~0ull << (lane + 1));
+    const int rq = later ? (__ffsll((unsigned long long)later) - 1) >> 2 : kWave / 4;
+    // segmented suffix min / max of the in-wave prefix extremes over [q, rq)
+    int64_t amn = zl + qmn, amx = zl + qmx;
+#pragma unroll
+    for (int d = 1; d < kWave / 4; d <<= 1) {
+        const int64_t omn = shfl_i64(amn, min(lane + 4 * d, kWave - 1));
+        const int64_t omx = shfl_i64(amx, min(lane + 4 * d, kWave - 1));
+        if (q + d < rq) {
+            amn = min(amn, omn);
+            amx = max(amx, omx);
+        }
+    }
+    const int64_t zr = shfl_i64(zl, 4 * min(rq, kWave / 4 - 1) + 3);
+    if (qd == 3) {
+        SumRec rc;
+        rc.mn = amn - zl;
+        rc.mx = amx - zl;
+        rc.dsum = (rq < kWave / 4 ? zr : wtot) - zl;
+        rc.be = be;
+        rc.rend = wv * (kWave / 4) + rq;
+        L.rec[wv * (kWave / 4) + q] = rc;
     }
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 9);
-    // 2. integer steps per block in its predicted binade
+    // c. the walk (wave 0, scalar control flow, every lane carries S)
+    if (wv == 0) {
+        const int nblk = (n + kSumBlk - 1) / kSumBlk;
+        // runs across waves: the head record of wave w (its run starts at the
+        // wave's first block) is extended over the following waves while each
+        // is one run with the same prediction -- a segmented suffix scan of
+        // (min, max, sum) over the heads, lanes w < NT/64
+        constexpr int NW = NT / kWave;
+        if (lane < NW) {
+            const SumRec h = L.rec[lane * (kWave / 4)];
+            const int32_t bnext = __shfl_down(h.be, 1, kWave);
+            const bool link = lane + 1 < NW && h.rend == (lane + 1) * (kWave / 4) && bnext == h.be;
+            const uint64_t brk = __ballot(!link) & ((1ull << NW) - 1);
+            const uint64_t atl = brk & (~0ull << lane);  // the first break at or after this wave
+            const int k = __ffsll((unsigned long long)atl) - 1;
+            int64_t mn = h.mn, mx = h.mx, ds = h.dsum;
+            int32_t re = h.rend;
 #pragma unroll
-    for (int it = 0; it < kIt; ++it) {
-        const int i0 = (tid + it * NT) * kTpt;
-        if (i0 >= span) continue;  // uniform per quad
-        const int b = i0 / kSumBlk;
-        int e;
-        int64_t mdummy;
-        const bool fast = binade_of(sc.approx[b], e, mdummy);
-        const double sc52 = pow2(52 - (fast ? e : 0));
-        bool bad = !fast;
-        int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
-#pragma unroll
-        for (int j = 0; j < kTpt; ++j) {
-            int64_t d = 0;
-            if (fast && i0 + j < n) {
-                const double q = sel[i0 + j] * sc52;
-                const bool bj = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
-                bad |= bj;
-                d = bj ? 0 : (int64_t)rint(q);
+            for (int d = 1; d < NW; d <<= 1) {
+                const int src = min(lane + d, NW - 1);
+                const int64_t omn = shfl_i64(mn, src), omx = shfl_i64(mx, src), ods = shfl_i64(ds, src);
+                const int32_t ore = __shfl(re, src, kWave);
+                if (lane + d <= k) {
+                    mn = min(mn, ds + omn);
+                    mx = max(mx, ds + omx);
+                    ds += ods;
+                    re = ore;
+                }
             }
-            P += d;
-            mn = min(mn, P);
-            mx = max(mx, P);
+            SumRec& hw = L.rec[lane * (kWave / 4)];
+            hw.mn = mn;
+            hw.mx = mx;
+            hw.dsum = ds;
+            hw.rend = re;
         }
-        // inclusive prefix of the lane totals over the quad
-        uint64_t inc = (uint64_t)P;
-        {
-            uint64_t t = dpp64<0x111>(0, inc);
-            inc += qd >= 1 ? t : 0;
-            t = dpp64<0x112>(0, inc);
-            inc += qd >= 2 ? t : 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#ifdef SGMM_STAMPS
+        unsigned long long n_iter = 0, n_slow = 0;
+#endif
+        // One lane walks (LDS reads return 1/64 of the data of a wave-wide
+        // broadcast read); each iteration is branch-free: the block's reference
+        // additions and the run check run side by side and a select keeps one,
+        // with both possible successors' records already requested.
+        constexpr int NB = NT / 4;
+        if (lane == 0 && nblk > 0) {
+            int pos = 0;
+            SumRec cur = L.rec[0];
+            do {
+#ifdef SGMM_STAMPS
+                ++n_iter;
+#endif
+                const double2* vp = reinterpret_cast<const double2*>(sel + pos * kSumBlk);
+                double2 v[kSumBlk / 2];
+#pragma unroll
+                for (int j = 0; j < kSumBlk / 2; ++j) v[j] = vp[j];
+                const int pn = pos + 1, pj = cur.rend;
+                const SumRec rn = L.rec[min(pn, NB - 1)];
+                const SumRec rj = L.rec[min(pj, NB - 1)];
+                int e;
+                int64_t M;
+                bool ok = binade_of(S, e, M) && cur.be == e;
+                ok = ok && (M > 0 ? (M + cur.mn >= kMLo && M + cur.mx <= kMHi)
+                                  : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi));
+                const double Sj = from_binade(M + cur.dsum, e);
+                double Ss = S;  // the reference way (the last block padded with -0.0)
+#pragma unroll
+                for (int j = 0; j < kSumBlk / 2; ++j) {
+                    Ss += v[j].x;
+                    Ss += v[j].y;
+                }
+#ifdef SGMM_STAMPS
+                n_slow += ok ? 0 : 1;
+#endif
+                S = ok ? Sj : Ss;
+                pos = ok ? pj : pn;
+                cur = ok ? rj : rn;
+            } while (pos < nblk);
+            L.S = S;
         }
-        const int64_t ex = (int64_t)(inc - (uint64_t)P);
-        int64_t qmn = mn + ex, qmx = mx + ex;
-        {
-            int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
-            qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
-            t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
-            qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
-            t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
-            qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
-            t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
-            qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
-        }
-        const uint64_t bl = __ballot(bad);
-        if (qd == 3) {
-            sc.be[b] = fast ? e : INT32_MIN;
-            sc.pend[b] = (int64_t)inc;
-            sc.pmin[b] = qmn;
-            sc.pmax[b] = qmx;
-            sc.bad[b] = ((bl >> (lane & ~3)) & 0xFu) != 0;
-        }
+#ifdef SGMM_STAMPS
+        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; }
+#endif
+        if (lane == 0 && nblk == 0) L.S = S;
     }
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 10);
-    // 3. the walk (wave 0; every lane carries the same S)
-    if (tid < kWave) {
-        uint64_t zcarry = 0;  // exclusive prefix of the block sums, wrapping
-        for (int b0 = 0; b0 < nblk; b0 += kWave) {
-            const int b = b0 + lane;
-            const uint64_t v = b < nblk ? (uint64_t)sc.pend[b] : 0;
-            const uint64_t inc = wave_scan_add(v);
-            if (b < nblk) sc.z[b] = zcarry + (inc - v);
-            zcarry += readlane64(inc, kWave - 1);
-        }
-        SGMM_STAMP(blockIdx.x, 11);
-#ifdef SGMM_STAMPS
-        unsigned long long n_iter = 0, n_slow = 0, slow_cyc = 0, fast_cyc = 0;
-#endif
-        for (int g0 = 0; g0 < nblk; g0 += kWave) {
-            const int lim = min(kWave, nblk - g0);
-            const int b = g0 + lane;
-            const bool inb = lane < lim;
-            const int eb = inb ? sc.be[b] : INT32_MIN;
-            const int64_t pe = inb ? sc.pend[b] : 0, pmn = inb ? sc.pmin[b] : 0, pmx = inb ? sc.pmax[b] : 0;
-            const uint64_t zb = inb ? sc.z[b] : 0;
-            const bool bd = inb ? sc.bad[b] != 0 : true;
-            const uint64_t live = lim == kWave ? ~0ull : ((1ull << lim) - 1);
-            int pos = 0;
-            while (pos < lim) {
-#ifdef SGMM_STAMPS
-                ++n_iter;
-                unsigned long long tf0_;
-                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tf0_) : "v"(S) : "memory");
-#endif
-                S = uniform_f64(S);  // wave-uniform: scalar control flow below
-                int f = pos, e;
-                int64_t M;
-                if (binade_of(S, e, M)) {
-                    // M at the start of this lane's block if blocks pos.. are all accepted
-                    const int64_t c = M + (int64_t)(zb - readlane64(zb, pos));
-                    const bool okp = c + pmn >= kMLo && c + pmx <= kMHi;
-                    const bool okn = c + pmx <= -kMLo && c + pmn >= -kMHi;
-                    const bool ok = lane < pos || (inb && eb == e && !bd && (M > 0 ? okp : okn));
-                    const uint64_t fails = __ballot(!ok) & live;
-                    f = fails ? __ffsll((unsigned long long)fails) - 1 : lim;
-                    if (f > pos) {
-                        const uint64_t ce = (uint64_t)(f < lim ? c : c + pe);
-                        S = from_binade((int64_t)readlane64(ce, f < lim ? f : lim - 1), e);
-                    }
-                }
-#ifdef SGMM_STAMPS
-                {
-                    unsigned long long tf1_;
-                    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tf1_) : "v"(S), "s"(f) : "memory");
-                    fast_cyc += tf1_ - tf0_;
-                }
-#endif
-                if (f < lim) {  // this block the reference way
-#ifdef SGMM_STAMPS
-                    ++n_slow;
-                    unsigned long long ts0_;
-                    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts0_)::"memory");
-#endif
-                    const int t0 = (g0 + f) * kSumBlk, m = min(kSumBlk, n - t0);
-                    double v[kSumBlk];  // all loads in flight before the dependent adds
-#pragma unroll
-                    for (int j = 0; j < kSumBlk; ++j) v[j] = sel[t0 + min(j, m - 1)];
-                    if (m == kSumBlk) {
-#pragma unroll
-                        for (int j = 0; j < kSumBlk; ++j) S += v[j];
-                    } else {
-                        for (int j = 0; j < m; ++j) S += v[j];
-                    }
-#ifdef SGMM_STAMPS
-                    {
-                        unsigned long long ts1_;
-                        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ts1_) : "v"(S) : "memory");
-                        slow_cyc += ts1_ - ts0_;
-                    }
-#endif
-                    pos = f + 1;
-                } else {
-                    pos = lim;
-                }
-            }
-        }
-        SGMM_STAMP(blockIdx.x, 12);
-#ifdef SGMM_STAMPS
-        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; g_stamps[blockIdx.x][15] = slow_cyc; g_stamps[blockIdx.x][7] = fast_cyc; }
-#endif
-    }
-    __syncthreads();
-    return S;
+    return L.S;
 }
 
 // ------------------------------------------------------------------ generation tail
@@ -793,369 +867,70 @@ static inline size_t step_lds_bytes(int threads, const StepArgs& sa) {
            sizeof(float) * (size_t)(sa.n_mm + (sa.master_adv ? sa.n_adv : 0));
 }
 
+// The episode's fitness record, stored write-through (sc1) by ONE lane of
+// the workgroup: the hand-off to the generation tail needs no release fence.
+__device__ __forceinline__ void store_record(double* fitness, int32_t* trades, int e, double f,
+                                             int32_t t) {
+    typedef __attribute__((address_space(1))) double gdouble;
+    typedef __attribute__((address_space(1))) int32_t gint;
+    __hip_atomic_store((gdouble*)(fitness + e), f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gint*)(trades + e), t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Thread 0 stored the workgroup's record with store_record.  It drains the
+// stores, takes an arrival ticket (agent-scope atomic); the workgroup that
+// draws the last ticket reads every record with sc1 loads (ga_step_dev
+// <HANDOFF = true>) -- MI355X_MICROARCH.md inter-workgroup visibility, row 1
+// -- runs the GA step and resets the ticket for the next launch.
 __device__ void generation_tail(const StepArgs& sa, const double* fitness, const int32_t* trades,
                                 unsigned char* lds, int* s_last) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int prev = __hip_atomic_fetch_add(&sa.st->arrivals, 1, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
         *s_last = prev == (int)gridDim.x - 1;
-        if (*s_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
     }
     __syncthreads();
     if (!*s_last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: loads after the ticket
+    SGMM_STAMP(blockIdx.x, 4);
+#ifdef SGMM_STAMPS
+    if (threadIdx.x == 0) g_stamps[4095][0] = g_stamps[blockIdx.x][4];
+#endif
     const int nt = blockDim.x;
     double* sv = reinterpret_cast<double*>(lds);
     int* si = reinterpret_cast<int*>(sv + 2 * nt);
     float* lm = reinterpret_cast<float*>(si + 2 * nt);
     float* la = lm + sa.n_mm;
-    ga_step_dev(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, ShardView{0, 0},
-                sa.master_mm, sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed, sa.history,
-                sa.hist_cap, nullptr, nullptr, 0, 0, sv, si, lm, la);
+    if (sa.P <= nt && sa.n_mm <= 16 * nt && sa.n_adv <= 16 * nt)
+        ga_step_fused<true>(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, sa.master_mm,
+                            sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed, sa.history,
+                            sa.hist_cap, sv, si, lm, la);
+    else
+        ga_step_dev<true>(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, ShardView{0, 0},
+                          sa.master_mm, sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed,
+                          sa.history, sa.hist_cap, nullptr, nullptr, 0, 0, sv, si, lm, la);
     if (threadIdx.x == 0) sa.st->arrivals = 0;
+    SGMM_STAMP(blockIdx.x, 5);
 }
 
 // ------------------------------------------------------------------ path scan (no adversary)
-// One workgroup (16 waves) per episode.
-//   1. wave 0: chunk start states from a wave-level scan of the chunk maps;
-//      all waves: the episode's prefix words -> LDS (one coalesced pass);
-//   2. all waves: per tick, state = one field of its prefix word; gather the
-//      reward of that state into LDS, count trades;
-//   3. the rewards' sequential float64 sum, bit-exact (exact_ordered_sum).
-// Episodes longer than kScanWin ticks are processed in windows.
-
+// One workgroup (16 waves) per episode, 4096-tick windows.
+//   1. wave 0: chunk start states from a wave-level scan of the chunk maps,
+//      and the episode's trades: each chunk's count along the path from its
+//      start state (8 bits per start state, written by the table);
+//   2. every thread: the rewards of its 4 ticks from the path plane of their
+//      chunk's start state (one coalesced row per chunk) -> LDS;
+//   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
 template <int NSM>
-__global__ __launch_bounds__(kScanThreads) void k_path_scan_maps(
-    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
-    const uint32_t* __restrict__ words, const uint32_t* __restrict__ cmaps,
+__global__ __launch_bounds__(kScanThreads) void k_path_scan(
+    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
+    const uint32_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
     const double* __restrict__ rew, double* __restrict__ fitness,
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
-    double* sel = reinterpret_cast<double*>(lds);                          // [kScanWin]
-    uint32_t* wl = reinterpret_cast<uint32_t*>(sel + kScanWin);            // [kScanWin]
-    uint8_t* start = reinterpret_cast<uint8_t*>(wl + kScanWin);            // [nch]
-    __shared__ double s_approx[kScanBlks];
-    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
-    __shared__ int32_t s_be[kScanBlks];
-    __shared__ uint64_t s_z[kScanBlks];
-    __shared__ uint8_t s_bad[kScanBlks];
-    __shared__ int red_trades;
-    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
-    const int e = blockIdx.x;
-    const int32_t T = ep.len[e];
-    const int nch = (T + kChunk - 1) / kChunk;
-    const int64_t so = ep.step_off[e];
-    const uint32_t cb = chunk_base(so, e);
-    const int tid = threadIdx.x, lane = tid & (kWave - 1);
-    if (tid == 0) red_trades = 0;
-    SGMM_STAMP(e, 0);
-    if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
-        uint32_t s = (uint32_t)(-inv_min);
-        for (int c0 = 0; c0 < nch; c0 += kWave) {
-            const int c = c0 + lane;
-            const uint32_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
-            uint32_t inc = m;
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const uint32_t before = __shfl_up(inc, d, kWave);
-                if (lane >= d) inc = map_then<NSM>(before, inc);
-            }
-            uint32_t excl = __shfl_up(inc, 1, kWave);
-            if (lane == 0) excl = kIdentityMap;
-            if (c < nch) start[c] = (uint8_t)map_get(excl, s);
-            s = map_get(__shfl(inc, kWave - 1, kWave), s);
-        }
-    }
-    SGMM_STAMP(e, 1);
-    int my_trades = 0;
-    double total = 0.0;
-    for (int w0 = 0; w0 < T; w0 += kScanWin) {
-        const int n = min(kScanWin, T - w0);
-        for (int i = tid; i < n; i += kScanThreads) wl[i] = words[so + w0 + i];
-        __syncthreads();
-        SGMM_STAMP(e, 2);
-        {   // every reward gather of a thread issued before its first write
-            constexpr int kMaxPass = kScanWin / kScanThreads;
-            double r[kMaxPass];
-            uint32_t stv[kMaxPass], wdv[kMaxPass];
-#pragma unroll
-            for (int p = 0; p < kMaxPass; ++p) {
-                const int i = tid + p * kScanThreads;
-                if (i < n) {
-                    wdv[p] = wl[i];
-                    stv[p] = map_get(wdv[p], start[(w0 + i) / kChunk]);
-                    r[p] = rew[stv[p] * ep.rs + so + w0 + i];
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < kMaxPass; ++p) {
-                const int i = tid + p * kScanThreads;
-                if (i < n) {
-                    sel[i] = r[p];
-                    my_trades += (wdv[p] >> (24 + stv[p])) & 1u;
-                }
-            }
-        }
-        __syncthreads();
-        SGMM_STAMP(e, 3);
-        total = exact_ordered_sum<kScanThreads>(sel, n, total, sc);
-        SGMM_STAMP(e, 4);
-    }
-    SGMM_STAMP(e, 5);
-    int wsum = my_trades;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
-    if (lane == 0 && wsum) atomicAdd(&red_trades, wsum);
-    __syncthreads();
-    if (tid == 0) {
-        const int tr = red_trades;
-        if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
-        fitness[e] = total;
-        trades_out[e] = tr;
-    }
-    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
-}
-
-// ------------------------------------------------------------------ exact ordered sum v2
-// The same exact sum as exact_ordered_sum, restructured around latency for a
-// 1024-thread workgroup whose threads hold the values in registers: thread
-// tid owns elements 4 tid .. 4 tid + 3 of a 4096-element window, so a 16-element
-// summation block is one quad of lanes.
-//   1. approximate block starts: a float32 wave scan + the waves' totals
-//      (one barrier);
-//   2. each block's predicted binade, its integer steps, their quad prefix
-//      range, the tie / huge flags, and the block sums' wave-level exclusive
-//      prefix -> per-block records in LDS (one barrier);
-//   3. wave 0 holds the records of blocks 64 j + lane in registers (4 per lane)
-//      and walks: each iteration is one masked range check per register slot
-//      and a scalar find-first; a failing block is added the reference way
-//      from the window's values in LDS (one barrier, S broadcast).
-// Every accepted shortcut is exact (see exact_ordered_sum), so the result is
-// the sequential float64 sum bit for bit.
-constexpr int kTpt2 = 4;                          // elements per thread
-constexpr int kWin2 = kScanThreads * kTpt2;       // elements per window
-constexpr int kBlk2 = kWin2 / kSumBlk;            // 16-element blocks per window
-constexpr int kWaves2 = kScanThreads / kWave;     // waves per workgroup
-constexpr int kSlots2 = kBlk2 / kWave;            // walk: blocks per lane
-static_assert(kSumBlk == 4 * kTpt2, "a block is one quad of lanes");
-static_assert(kSlots2 == 4, "pick4");
-
-// inclusive float32 prefix sum over the wave (DPP row shifts + row broadcasts)
-__device__ __forceinline__ float wave_scan_add_f32(float v) {
-#define SGMM_FSTEP2(CTRL, RM) \
-    v += __int_as_float((int)dpp32<CTRL, RM>(0u, (uint32_t)__float_as_int(v)));
-    SGMM_FSTEP2(0x111, 0xF) SGMM_FSTEP2(0x112, 0xF) SGMM_FSTEP2(0x114, 0xF)
-    SGMM_FSTEP2(0x118, 0xF) SGMM_FSTEP2(0x142, 0xA) SGMM_FSTEP2(0x143, 0xC)
-#undef SGMM_FSTEP2
-    return v;
-}
-
-template <typename V>
-__device__ __forceinline__ V pick4(const V (&a)[kSlots2], int j) {  // j wave-uniform
-    return j == 0 ? a[0] : j == 1 ? a[1] : j == 2 ? a[2] : a[3];
-}
-
-struct SumLds2 {
-    double sel[kWin2];  // the window's values (fallback blocks)
-    int32_t be[kBlk2];  // predicted binade (INT32_MIN: none / tie / huge step)
-    int64_t mn[kBlk2], mx[kBlk2];  // range of the block's inclusive integer prefixes
-    uint64_t z[kBlk2];  // wave-local exclusive prefix of the block sums
-    float w_ap[kWaves2];
-    uint64_t w_z[kWaves2];
-    double S;
-};
-
-// All kScanThreads threads call after L.sel[0, n) holds the window's values
-// and a barrier; returns S + sel[0] + ... + sel[n-1] in sequential float64
-// order in every thread.  S must be identical in every thread.  Ends with a
-// barrier (L.sel may then be refilled).
-__device__ __forceinline__ double exact_sum_window(int n, double S, SumLds2& L) {
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6, qd = lane & 3;
-    const int i0 = tid * kTpt2;
-    double r[kTpt2];
-#pragma unroll
-    for (int j = 0; j < kTpt2; ++j) r[j] = i0 + j < n ? L.sel[i0 + j] : 0.0;
-    // 1. approximate block starts (only binade predictions: float32 is enough)
-    const float fv = (float)(((r[0] + r[1]) + r[2]) + r[3]);
-    const float finc = wave_scan_add_f32(fv);
-    const float fbs = __int_as_float((int)dpp32<0x00>(0u, (uint32_t)__float_as_int(finc - fv)));
-    if (lane == kWave - 1) L.w_ap[wv] = finc;
-    __syncthreads();
-    SGMM_STAMP(blockIdx.x, 8);
-    float woff = 0.0f;  // the preceding waves' totals (broadcast reads, in order)
-#pragma unroll
-    for (int k = 0; k < kWaves2; ++k) woff += k < wv ? L.w_ap[k] : 0.0f;
-    // 2. integer steps of the block in its predicted binade
-    int eb;
-    int64_t mdummy;
-    const bool fast = binade_of(S + (double)(woff + fbs), eb, mdummy);
-    const double sc52 = pow2(52 - (fast ? eb : 0));
-    bool bad = !fast;
-    int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
-#pragma unroll
-    for (int j = 0; j < kTpt2; ++j) {
-        int64_t d = 0;
-        if (fast && i0 + j < n) {
-            const double q = r[j] * sc52;
-            const bool bj = !(fabs(q) < 0x1p56) || (q - floor(q) == 0.5);
-            bad |= bj;
-            d = bj ? 0 : (int64_t)rint(q);
-        }
-        P += d;
-        mn = min(mn, P);
-        mx = max(mx, P);
-    }
-    uint64_t qinc = (uint64_t)P;  // inclusive prefix of the lane totals over the quad
-    {
-        uint64_t t = dpp64<0x111>(0, qinc);
-        qinc += qd >= 1 ? t : 0;
-        t = dpp64<0x112>(0, qinc);
-        qinc += qd >= 2 ? t : 0;
-    }
-    const int64_t ex = (int64_t)(qinc - (uint64_t)P);
-    int64_t qmn = mn + ex, qmx = mx + ex;
-    {
-        int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
-        qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
-        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
-        qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
-        t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
-        qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
-        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
-        qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
-    }
-    const uint64_t bl = __ballot(bad);
-    const uint64_t bt = qd == 3 ? qinc : 0;  // block total at the quad's last lane
-    const uint64_t zinc = wave_scan_add(bt);
-    if (lane == kWave - 1) L.w_z[wv] = zinc;
-    if (qd == 3) {
-        const int b = wv * (kWave / 4) + (lane >> 2);
-        L.be[b] = (fast && ((bl >> (lane & ~3)) & 0xFu) == 0) ? eb : INT32_MIN;
-        L.mn[b] = qmn;
-        L.mx[b] = qmx;
-        L.z[b] = zinc - bt;
-    }
-    __syncthreads();
-    SGMM_STAMP(blockIdx.x, 9);
-    // 3. the walk (wave 0; every lane carries the same S)
-    if (wv == 0) {
-        const uint64_t wz = lane < kWaves2 ? L.w_z[lane] : 0;
-        const uint64_t wzi = wave_scan_add(wz);
-        const uint64_t zend = readlane64(wzi, kWave - 1);
-        const uint64_t wzx = wzi - wz;  // exclusive prefix of the wave totals
-        const int nblk = (n + kSumBlk - 1) / kSumBlk;
-        int ber[kSlots2];
-        int64_t mnr[kSlots2], mxr[kSlots2];
-        uint64_t zr[kSlots2];
-#pragma unroll
-        for (int j = 0; j < kSlots2; ++j) {
-            const int b = kWave * j + lane;
-            const int src = b / (kWave / 4);  // the wave that produced block b
-            const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)wzx, src, kWave);
-            const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(wzx >> 32), src, kWave);
-            ber[j] = L.be[b];
-            mnr[j] = L.mn[b];
-            mxr[j] = L.mx[b];
-            zr[j] = L.z[b] + (((uint64_t)hi << 32) | lo);
-        }
-        SGMM_STAMP(blockIdx.x, 10);
-#ifdef SGMM_STAMPS
-        unsigned long long n_iter = 0, n_slow = 0, c_fast = 0, c_slow = 0, t_a, t_b, t_c;
-#endif
-        int pos = 0;
-        while (pos < nblk) {
-#ifdef SGMM_STAMPS
-            ++n_iter;
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_a) : "v"(S) : "memory");
-#endif
-            S = uniform_f64(S);  // wave-uniform: scalar control flow below
-            int f = pos, eS;
-            int64_t M;
-            if (binade_of(S, eS, M)) {
-                // M at the start of block b if blocks pos .. b-1 are all accepted: K + z[b]
-                const uint64_t K = (uint64_t)M - readlane64(pick4(zr, pos / kWave), pos % kWave);
-                f = nblk;
-#pragma unroll
-                for (int j = 0; j < kSlots2; ++j) {
-                    if (f == nblk && kWave * j < nblk && kWave * (j + 1) > pos) {
-                        const int b = kWave * j + lane;
-                        const uint64_t c = K + zr[j];
-                        const int64_t lo = (int64_t)(c + (uint64_t)mnr[j]);
-                        const int64_t hi = (int64_t)(c + (uint64_t)mxr[j]);
-                        const bool inr = M > 0 ? (lo >= kMLo && hi <= kMHi) : (hi <= -kMLo && lo >= -kMHi);
-                        const bool ok = b < pos || b >= nblk || (ber[j] == eS && inr);
-                        const uint64_t fails = __ballot(!ok);
-                        if (fails) f = kWave * j + __ffsll((unsigned long long)fails) - 1;
-                    }
-                }
-                if (f > pos) {
-                    const uint64_t zf = f < nblk ? readlane64(pick4(zr, f / kWave), f % kWave) : zend;
-                    S = from_binade((int64_t)(K + zf), eS);
-                }
-            }
-#ifdef SGMM_STAMPS
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_b) : "v"(S), "s"(f) : "memory");
-            c_fast += t_b - t_a;
-#endif
-            if (f < nblk) {  // this block the reference way
-#ifdef SGMM_STAMPS
-                ++n_slow;
-#endif
-                const int t0 = f * kSumBlk, m = min(kSumBlk, n - t0);
-                double v[kSumBlk];
-#pragma unroll
-                for (int j = 0; j < kSumBlk; ++j) v[j] = L.sel[t0 + min(j, m - 1)];
-                if (m == kSumBlk) {
-#pragma unroll
-                    for (int j = 0; j < kSumBlk; ++j) S += v[j];
-                } else {  // the window's last block
-#pragma unroll
-                    for (int j = 0; j < kSumBlk; ++j)
-                        if (j < m) S += v[j];
-                }
-                pos = f + 1;
-#ifdef SGMM_STAMPS
-                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_c) : "v"(S) : "memory");
-                c_slow += t_c - t_b;
-#endif
-            } else {
-                pos = nblk;
-            }
-        }
-        SGMM_STAMP(blockIdx.x, 11);
-#ifdef SGMM_STAMPS
-        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; g_stamps[blockIdx.x][15] = c_fast; g_stamps[blockIdx.x][7] = c_slow; }
-#endif
-        if (lane == 0) L.S = S;
-    }
-    __syncthreads();
-    return L.S;
-}
-
-// ------------------------------------------------------------------ path scan v2 (no adversary)
-// The same result as k_path_scan_maps, restructured around latency: one
-// workgroup (16 waves) per episode, 4096-tick windows.
-//   0. loads issued at entry, before anything waits: wave 0's chunk maps, then
-//      every thread's prefix words and all ns rewards (SoA rows) of ticks
-//      tid + 1024 p -- each load instruction reads 512 contiguous bytes;
-//   1. wave 0: chunk start states -> LDS                             [barrier]
-//   2. per tick: state, selected reward (register select) -> LDS, traded bit
-//                                                                    [barrier]
-//   3. exact_sum_window on the selected rewards         [3 barriers per window]
-template <int NSM>
-__global__ __launch_bounds__(kScanThreads) void k_path_scan_v2(
-    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
-    const uint32_t* __restrict__ words, const uint32_t* __restrict__ cmaps,
-    const double* __restrict__ rew, double* __restrict__ fitness,
-    int32_t* __restrict__ trades_out, StepArgs step) {
-    extern __shared__ __align__(16) unsigned char lds[];
-    SumLds2& L = *reinterpret_cast<SumLds2*>(lds);
+    double* sel = reinterpret_cast<double*>(lds);  // [kScanWin]
+    __shared__ SumLds<kScanThreads> L;
     __shared__ uint8_t start[kMaxLen / kChunk];
     __shared__ int red_trades;
     const int e = blockIdx.x;
@@ -1163,32 +938,15 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_v2(
     const int nch = (T + kChunk - 1) / kChunk;
     const int64_t so = ep.step_off[e];
     const uint32_t cb = chunk_base(so, e);
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
-    const int ns = nsi;
-    if (tid == 0) red_trades = 0;
-
-    // ---- 0. loads: wave 0's first chunk maps, then every thread's window-0 data
-    const uint32_t cm0 = (wv == 0 && lane < nch) ? cmaps[cb + lane] : kIdentityMap;
-    uint32_t wd[kTpt2];
-    double rv[kTpt2][NSM];
-#define SGMM_LOAD_WINDOW(W0, N)                                                    \
-    _Pragma("unroll") for (int p = 0; p < kTpt2; ++p) {                            \
-        const int i = p * kScanThreads + tid;                                      \
-        wd[p] = 0;                                                                 \
-        if (i < (N)) {                                                             \
-            wd[p] = words[so + (W0) + i];                                          \
-            _Pragma("unroll") for (int s = 0; s < NSM; ++s)                        \
-                rv[p][s] = s < ns ? rew[s * ep.rs + so + (W0) + i] : 0.0;          \
-        }                                                                          \
-    }
+    const int tid = threadIdx.x, lane = tid & (kWave - 1);
     SGMM_STAMP(e, 0);
-    SGMM_LOAD_WINDOW(0, min(kWin2, T))
-    // ---- 1. chunk start states (wave 0), 64 chunks per round
-    if (wv == 0) {
+    if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
         uint32_t s = (uint32_t)(-inv_min);
+        int tr = 0;
         for (int c0 = 0; c0 < nch; c0 += kWave) {
             const int c = c0 + lane;
-            const uint32_t m = c0 == 0 ? cm0 : (c < nch ? cmaps[cb + c] : kIdentityMap);
+            const uint32_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
+            const uint64_t k = c < nch ? ctr[cb + c] : 0;
             uint32_t inc = m;
 #pragma unroll
             for (int d = 1; d < kWave; d <<= 1) {
@@ -1197,91 +955,60 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan_v2(
             }
             uint32_t excl = __shfl_up(inc, 1, kWave);
             if (lane == 0) excl = kIdentityMap;
-            if (c < nch) start[c] = (uint8_t)map_get(excl, s);
+            const uint32_t st = map_get(excl, s);
+            if (c < nch) start[c] = (uint8_t)st;
+            tr += (int)((k >> (8 * st)) & 0xFFu);
             s = map_get(__shfl(inc, kWave - 1, kWave), s);
         }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, kWave);
+        if (lane == 0) red_trades = tr;
     }
-    SGMM_STAMP(e, 1);
     __syncthreads();
-    SGMM_STAMP(e, 2);
-
-    int my_trades = 0;
+    SGMM_STAMP(e, 1);
     double S = 0.0;  // exact running sum (identical in every thread between windows)
-    for (int w0 = 0; w0 < T; w0 += kWin2) {
-        const int n = min(kWin2, T - w0);
-        if (w0 > 0) {
-            SGMM_LOAD_WINDOW(w0, n)
-        }
-        // ---- 2. states and selected rewards (a wave's 64 ticks are one chunk)
+    for (int w0 = 0; w0 < T; w0 += kScanWin) {
+        const int n = min(kScanWin, T - w0);
+        const int i0 = tid * kSumTpt;
+        if (i0 < n) {  // 4 ticks of one chunk (kChunk % kSumTpt == 0)
+            const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
+            double r[kSumTpt];
 #pragma unroll
-        for (int p = 0; p < kTpt2; ++p) {
-            const int i = p * kScanThreads + tid;
-            if (i < n) {
-                const uint32_t st = map_get(wd[p], start[(w0 + i) / kChunk]);
-                double x = rv[p][0];
+            for (int j = 0; j < kSumTpt; ++j) r[j] = src[min(j, n - 1 - i0)];
 #pragma unroll
-                for (int s = 1; s < NSM; ++s) x = st == (uint32_t)s ? rv[p][s] : x;
-                L.sel[i] = x;
-                my_trades += (wd[p] >> (24 + st)) & 1u;
-            }
+            for (int j = 0; j < kSumTpt; ++j)
+                if (i0 + j < n) sel[i0 + j] = r[j];
         }
         __syncthreads();
-        SGMM_STAMP(e, 3);
-        // ---- 3. the window's exact sum
-        S = exact_sum_window(n, S, L);
-        SGMM_STAMP(e, 4);
+        SGMM_STAMP(e, 2);
+        S = exact_sum_window<kScanThreads>(sel, n, S, L);
     }
-#undef SGMM_LOAD_WINDOW
-    int wsum = my_trades;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) wsum += __shfl_xor(wsum, off, kWave);
-    if (lane == 0 && wsum) atomicAdd(&red_trades, wsum);
-    __syncthreads();
+    SGMM_STAMP(e, 3);
     if (tid == 0) {
         const int tr = red_trades;
         double total = S;
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
-        fitness[e] = total;
-        trades_out[e] = tr;
+        store_record(fitness, trades_out, e, total, tr);
     }
-    SGMM_STAMP(e, 5);
     if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
-}
-
-// ordered sum through exact_sum_window (sgmm_ordered_sum's default kernel)
-__global__ __launch_bounds__(kScanThreads) void k_ordered_sum_v2(const double* __restrict__ x, int64_t n,
-                                                                 double init, double* __restrict__ out) {
-    __shared__ SumLds2 L;
-    double S = init;
-    for (int64_t w0 = 0; w0 < n; w0 += kWin2) {
-        const int m = (int)min((int64_t)kWin2, n - w0);
-        for (int i = threadIdx.x; i < m; i += kScanThreads) L.sel[i] = x[w0 + i];
-        __syncthreads();
-        S = exact_sum_window(m, S, L);
-    }
-    if (threadIdx.x == 0) *out = S;
 }
 
 // ------------------------------------------------------------------ ordered sum (standalone)
 // init + x[0] + x[1] + ... in sequential float64 order, one workgroup.
 __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __restrict__ x, int64_t n,
                                                               double init, double* __restrict__ out) {
-    __shared__ double sel[kScanWin];
-    __shared__ double s_approx[kScanBlks];
-    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
-    __shared__ int32_t s_be[kScanBlks];
-    __shared__ uint64_t s_z[kScanBlks];
-    __shared__ uint8_t s_bad[kScanBlks];
-    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
+    __shared__ __align__(16) double sel[kScanWin];
+    __shared__ SumLds<kScanThreads> L;
     double S = init;
     for (int64_t w0 = 0; w0 < n; w0 += kScanWin) {
         const int m = (int)min((int64_t)kScanWin, n - w0);
         for (int i = threadIdx.x; i < m; i += kScanThreads) sel[i] = x[w0 + i];
         __syncthreads();
-        S = exact_ordered_sum<kScanThreads>(sel, m, S, sc);
+        S = exact_sum_window<kScanThreads>(sel, m, S, L);
     }
     if (threadIdx.x == 0) *out = S;
 }
+
 
 // ------------------------------------------------------------------ path scan (adversary)
 // 20-state transducer (inventory x previous fills): every chunk is walked from
@@ -1298,12 +1025,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     double* __restrict__ fitness, int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);
-    __shared__ double s_approx[kScanBlks];
-    __shared__ int64_t s_pend[kScanBlks], s_pmin[kScanBlks], s_pmax[kScanBlks];
-    __shared__ int32_t s_be[kScanBlks];
-    __shared__ uint64_t s_z[kScanBlks];
-    __shared__ uint8_t s_bad[kScanBlks];
-    const SumScratch sc{s_approx, s_be, s_pend, s_pmin, s_pmax, s_z, s_bad};
+    __shared__ SumLds<kScanBlock> L;
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
     const int ns = 4 * nsi;
@@ -1349,7 +1071,8 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
             }
         }
         __syncthreads();
-        total = exact_ordered_sum<kScanBlock>(sel, segn, total, sc);
+        for (int k = 0; k < segn; k += 4 * kScanBlock)  // windows of 4 values per thread
+            total = exact_sum_window<kScanBlock>(sel + k, min(4 * kScanBlock, segn - k), total, L);
     }
     int w = my_trades;
 #pragma unroll
@@ -1359,8 +1082,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     if (tid == 0) {
         const int tr = red_trades;
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;
-        fitness[e] = total;
-        trades_out[e] = tr;
+        store_record(fitness, trades_out, e, total, tr);
     }
     if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
 }
@@ -1573,14 +1295,6 @@ static int table_path() {
     return (e && std::strcmp(e, "valu") == 0) ? 1 : 0;
 }
 
-// Path-scan kernel selection: 1 = the windowed k_path_scan_maps (default),
-// 0 = k_path_scan_v2 (SGMM_SCAN=v2; A/B measurements and a cross-check in the
-// tests -- it loads all ns rewards per tick up front, which measured slower).
-static int scan_path() {
-    const char* e = std::getenv("SGMM_SCAN");
-    return (e && std::strcmp(e, "v2") == 0) ? 0 : 1;
-}
-
 }  // namespace sgmm
 
 using namespace sgmm;
@@ -1589,42 +1303,43 @@ using namespace sgmm;
 extern "C" int sgmm_debug_stamps(unsigned long long* host, int n_eps) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 16 * n_eps);
 }
+extern "C" int sgmm_debug_tail(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 8);
+}
 extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * n_waves);
 }
 #endif
 
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
-//   u32 words[total_steps] | u32 cmaps[total_steps/64 + n + 1] (no adversary)
-//   u64 fills[total_steps]                                  (adversary)
-//   f64 rew: no adversary [n_states][rs] (rs = total_steps rounded up to 32),
-//            adversary [total_steps][n_states]
-static size_t ws_words(int64_t steps) { return align256((size_t)steps * sizeof(uint32_t)); }
-static size_t ws_cmaps(int32_t n, int64_t steps) {
-    return align256(((size_t)steps / kChunk + (size_t)n + 1) * sizeof(uint32_t));
-}
+//   no adversary: u32 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
+//                 slots) | f64 path planes rew[n_states][rs] (rs = total_steps
+//                 rounded up to 32)
+//   adversary:    u64 fills[total_steps] | f64 rew[total_steps][n_states]
+static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
+static size_t ws_cmaps(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint32_t)); }
+static size_t ws_ctr(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint64_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
                                               int32_t n_states) {
     if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
-    const size_t head = n_states > 8 ? ws_fills(total_steps)
-                                     : ws_words(total_steps) + ws_cmaps(n_episodes, total_steps);
     if (n_states > 8)  // adversary: rew[row * n_states + state]
-        return head + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
-    return head + (size_t)rew_stride(total_steps) * (size_t)n_states * sizeof(double);
+        return ws_fills(total_steps) + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
+    return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) +
+           (size_t)rew_stride(total_steps) * (size_t)n_states * sizeof(double);
 }
 
 template <int H>
 static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
                               const sgmm_ticks& tk, const EpArrays& ep,
                               const sgmm_env_params* params, const GenomeSrc& src, int32_t inv_min,
-                              uint32_t* words, uint32_t* cmaps, uint64_t* fills, double* rew) {
+                              uint64_t* ctr, uint32_t* cmaps, uint64_t* fills, double* rew) {
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
 #define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
     hipLaunchKernelGGL((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
-                       src, inv_min, nsi, words, cmaps, fills, rew)
+                       src, inv_min, nsi, ctr, cmaps, fills, rew)
     if (arl) {
         if (nsi <= 5) SGMM_TABLE_MFMA(5, true);
         else SGMM_TABLE_MFMA(8, true);
@@ -1639,12 +1354,12 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
 template <int H>
 static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm_ticks& tk,
                          const EpArrays& ep, const sgmm_env_params* params, const GenomeSrc& src,
-                         int32_t inv_min, uint32_t* words, uint32_t* cmaps, uint64_t* fills,
+                         int32_t inv_min, uint64_t* ctr, uint32_t* cmaps, uint64_t* fills,
                          double* rew) {
     const dim3 block(kChunk * nsi);  // one wave per inventory state
 #define SGMM_TABLE(NSM_, ARL_)                                                                  \
     hipLaunchKernelGGL((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, src, \
-                       inv_min, nsi, words, cmaps, fills, rew)
+                       inv_min, nsi, ctr, cmaps, fills, rew)
     if (arl) SGMM_TABLE(8, true);
     else if (nsi <= 5) SGMM_TABLE(5, false);
     else SGMM_TABLE(8, false);
@@ -1656,12 +1371,8 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
     clear_error();
     SGMM_REQUIRE(out && (values || n == 0) && n >= 0, "bad arguments");
     ProfScope prof("ordered_sum", as_stream(stream));
-    if (scan_path() == 0)
-        hipLaunchKernelGGL(k_ordered_sum_v2, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values,
-                           n, init, out);
-    else
-        hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
-                           init, out);
+    hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
+                       init, out);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }
@@ -1681,7 +1392,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         return SGMM_ERR_WORKSPACE;
     }
     char* w = reinterpret_cast<char*>(workspace);
-    uint32_t* words = nullptr;
+    uint64_t* ctr = nullptr;
     uint32_t* cmaps = nullptr;
     uint64_t* fills = nullptr;
     double* rew;
@@ -1689,10 +1400,10 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         fills = reinterpret_cast<uint64_t*>(w);
         rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
     } else {
-        words = reinterpret_cast<uint32_t*>(w);
-        cmaps = reinterpret_cast<uint32_t*>(w + ws_words(eps->total_steps));
-        rew = reinterpret_cast<double*>(w + ws_words(eps->total_steps) +
-                                        ws_cmaps(eps->n, eps->total_steps));
+        cmaps = reinterpret_cast<uint32_t*>(w);
+        ctr = reinterpret_cast<uint64_t*>(w + ws_cmaps(eps->n, eps->total_steps));
+        rew = reinterpret_cast<double*>(w + ws_cmaps(eps->n, eps->total_steps) +
+                                        ws_ctr(eps->n, eps->total_steps));
     }
     const EpArrays ep = ep_arrays(eps, arl);
     if (eps->max_len > 0) {
@@ -1700,18 +1411,18 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ProfScope prof("policy_table", s);
         const bool valu = table_path() == 1;
         switch (hidden) {
-            case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew); break;
+            case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew); break;
             case 16:
-                if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
+                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
                 break;
             case 32:
-                if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
+                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
                 break;
             default:
-                if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
-                else launch_table_mfma<64>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, words, cmaps, fills, rew);
+                if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
+                else launch_table_mfma<64>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
                 break;
         }
         SGMM_LAUNCHED();
@@ -1724,26 +1435,14 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         hipLaunchKernelGGL(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
-        if (scan_path() == 0) {
-            size_t lds = sizeof(SumLds2);
-            if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
-            if (nsi <= 5)
-                hipLaunchKernelGGL(k_path_scan_v2<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                                   params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
-            else
-                hipLaunchKernelGGL(k_path_scan_v2<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                                   params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
-            SGMM_LAUNCHED();
-            return SGMM_OK;
-        }
-        size_t lds = kScanWin * (sizeof(double) + sizeof(uint32_t)) + nch_max;
+        size_t lds = kScanWin * sizeof(double);
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
         if (nsi <= 5)
-            hipLaunchKernelGGL(k_path_scan_maps<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
+            hipLaunchKernelGGL(k_path_scan<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
+                               eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
         else
-            hipLaunchKernelGGL(k_path_scan_maps<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep,
-                               params, eps->inv_min, nsi, words, cmaps, rew, fitness, trades, step);
+            hipLaunchKernelGGL(k_path_scan<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
+                               eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
     }
     SGMM_LAUNCHED();
     return SGMM_OK;

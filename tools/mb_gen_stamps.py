@@ -49,12 +49,26 @@ print(f"  wave start ns: {q((h[:, 7] - real0) * 10)}; last end ns {((h[:, 6] - r
 s = np.zeros((n_ep, 16), np.uint64)
 L.sgmm_debug_stamps(s.ctypes.data, n_ep)
 s = s.astype(np.int64)
-ds = s[:, 1:6] - s[:, [0]]
-print(f"scan (train episodes, median): chunk-starts {np.median(ds[:P,0]):.0f} words {np.median(ds[:P,1]):.0f} "
-      f"gathered {np.median(ds[:P,2]):.0f} summed {np.median(ds[:P,3]):.0f} end {np.median(ds[:P,4]):.0f}")
+rel = lambda k, sl: np.median(s[sl, k] - s[sl, 0])
+print(f"scan (train episodes, median): chunk-starts {rel(1, slice(0, P)):.0f} rewards {rel(2, slice(0, P)):.0f} "
+      f"records {rel(9, slice(0, P)):.0f} walk-done {rel(10, slice(0, P)):.0f} end {rel(3, slice(0, P)):.0f}")
 print(f"scan walk: iterations med {np.median(s[:P,13]):.0f} max {s[:P,13].max()}, slow med {np.median(s[:P,14]):.0f} max {s[:P,14].max()}")
 print(f"scan walk val eps: iterations med {np.median(s[P:,13]):.0f} max {s[P:,13].max()}, slow med {np.median(s[P:,14]):.0f} max {s[P:,14].max()}")
-dd = s[:, 5] - s[:, 0]
+last = np.nonzero(s[:, 5] > s[:, 0])[0]
+if len(last):
+    k = last[0]
+    print(f"generation tail (last-arriving episode {k}): arrival {s[k, 4] - s[k, 0]} cycles after its entry, "
+          f"tail {s[k, 5] - s[k, 4]} cycles; first scan entry -> tail end {s[k, 5] - s[:, 0].min()} cycles")
+L.sgmm_debug_tail.argtypes = [ctypes.c_void_p]
+tl = np.zeros(8, np.uint64)
+L.sgmm_debug_tail(tl.ctypes.data)
+tl = tl.astype(np.int64)
+s4k = np.zeros((4096, 16), np.uint64)
+L.sgmm_debug_stamps(s4k.ctypes.data, 4096)
+t0 = int(s4k[4095, 0])
+print("tail phases (cycles from the ticket): loads", tl[0] - t0, "shuffles", tl[6] - t0, "barrier", tl[7] - t0,
+      "argmax", tl[1] - t0, "regen", tl[2] - t0, "barrier", tl[3] - t0, "bookkeeping", tl[4] - t0, "best copy", tl[5] - t0)
+dd = s[:, 3] - s[:, 0]
 print("scan total cycles per episode: train med", np.median(dd[:P]), "max", dd[:P].max(), "val med", np.median(dd[P:]), "max", dd[P:].max())
 hist = sess.hist[:GENS].cpu().numpy().view(sg.drl_engine.HIST_DTYPE).reshape(-1)
 print("train_f", hist["train_f"], "val_f", hist["val_f"])

@@ -1,6 +1,6 @@
 """Diagnostic: sgmm_ordered_sum on the bench workload's real selected rewards
 (oracle trace of one P=64 bench episode, H=16, T=3600).  Prints us per call
-(HIP events) for the kernel SGMM_SCAN selects; with the stamped library
+(HIP events) with the stamped library
 (SGMM_LIB=tools/mb/libsgmm_stamps.so) also the v2 phase cycles."""
 import ctypes
 import os
@@ -37,12 +37,11 @@ torch.cuda.synchronize()
 seq = 0.0
 for v in x:
     seq += v
-print(os.environ.get("SGMM_SCAN", "v2"), os.path.basename(os.environ.get("SGMM_LIB", "libsgmm.so")),
+print(os.path.basename(os.environ.get("SGMM_LIB", "libsgmm.so")),
       "us per call %.2f" % (e0.elapsed_time(e1) * 1e3 / 100), "exact", out.item() == seq)
 if "stamps" in os.environ.get("SGMM_LIB", ""):
     L.sgmm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     h = np.zeros((1, 16), np.uint64)
     L.sgmm_debug_stamps(h.ctypes.data, 1)
     h = h.astype(np.int64)[0]
-    print("  cycles: approx->records %d, records->walk %d, walk %d (fast checks %d, fallback adds %d); "
-          "iterations %d fallback %d" % (h[9] - h[8], h[10] - h[9], h[11] - h[10], h[15], h[7], h[13], h[14]))
+    print("  cycles: approx->records %d, walk %d; iterations %d fallback %d" % (h[9] - h[8], h[10] - h[9], h[13], h[14]))
