@@ -108,21 +108,38 @@ __device__ void stage_genomes(const GenomeSrc& src, int gi, int ai, int n, float
 
 // ------------------------------------------------------------------ transition maps
 // A step's effect on the (<= 8) inventory states is a map state -> state,
-// packed 3 bits per state in a u32 (bits 0..23).  Composition is cheap VALU
-// work, so a wave of 64 ticks builds the exclusive prefix of its chunk with
-// log2(64) shuffle rounds and the scan kernel reads every tick's state with
-// one field lookup.
-constexpr uint32_t kIdentityMap = 0xFAC688u;  // x -> x for x = 0..7
+// one byte per state in a u64 (byte x = image of state x).  Composition is
+// two v_perm_b32 (byte x of the result = byte a[x] of b), so a wave of 64
+// ticks builds the inclusive prefix of its chunk with six DPP steps and the
+// path of any start state is one byte lookup.
+constexpr uint64_t kIdentityMap = 0x0706050403020100ull;  // x -> x for x = 0..7
 
-__device__ __forceinline__ uint32_t map_get(uint32_t m, uint32_t x) { return (m >> (3u * x)) & 7u; }
+__device__ __forceinline__ uint32_t map_get(uint64_t m, uint32_t x) {
+    return (uint32_t)(m >> (8u * x)) & 0xFFu;
+}
 
-// "first a, then b" on the first NSM states
-template <int NSM>
-__device__ __forceinline__ uint32_t map_then(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int x = 0; x < NSM; ++x) r |= map_get(b, map_get(a, x)) << (3 * x);
-    return r;
+// "first a, then b": (a ; b)[x] = b[a[x]]
+__device__ __forceinline__ uint64_t map_then(uint64_t a, uint64_t b) {
+    const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint32_t lo = __builtin_amdgcn_perm(bh, bl, (uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_perm(bh, bl, (uint32_t)(a >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// inclusive prefix composition over the wave (row shifts, then row
+// broadcasts; a lane without a source composes the identity)
+__device__ __forceinline__ uint64_t wave_map_scan(uint64_t m) {
+#define SGMM_MSTEP(CTRL, RM) m = map_then(dpp64<CTRL, RM>(kIdentityMap, m), m);
+    SGMM_MSTEP(0x111, 0xF) SGMM_MSTEP(0x112, 0xF) SGMM_MSTEP(0x114, 0xF)
+    SGMM_MSTEP(0x118, 0xF) SGMM_MSTEP(0x142, 0xA) SGMM_MSTEP(0x143, 0xC)
+#undef SGMM_MSTEP
+    return m;
+}
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, kWave);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, kWave);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 __device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
@@ -150,7 +167,7 @@ template <int H, int NSM, bool ARL>
 __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
     GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
-    uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
+    uint64_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
     const int32_t t0 = blockIdx.x * kChunk;
@@ -234,23 +251,19 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
         }
         return;
     }
-    uint32_t map = kIdentityMap, traded = 0;
+    uint64_t map = kIdentityMap;
+    uint32_t traded = 0;
     if (valid) {
-        map = 0;
         for (int s = 0; s < nsi; ++s) {
             const uint32_t c = code[s][lane];
-            map |= (uint32_t)(s + (int)(c & 1u) - (int)(c >> 1)) << (3 * s);
+            const uint64_t to = (uint64_t)(s + (int)(c & 1u) - (int)(c >> 1));
+            map = (map & ~(0xFFull << (8 * s))) | (to << (8 * s));
             traded |= (uint32_t)(c != 0) << s;
         }
     }
-    // exclusive prefix of the chunk's step maps (Hillis-Steele over the wave)
-    uint32_t inc = map;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t before = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc = map_then<NSM>(before, inc);
-    }
-    uint32_t excl = __shfl_up(inc, 1, kWave);
+    // exclusive prefix of the chunk's step maps
+    const uint64_t inc = wave_map_scan(map);
+    uint64_t excl = shfl_up_u64(inc, 1);
     if (lane == 0) excl = kIdentityMap;
     uint64_t cnt = 0;
     for (int s0 = 0; s0 < nsi; ++s0) {
@@ -328,7 +341,7 @@ template <int H, int NSI, bool ARL>
 __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfma(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
     GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
-    uint32_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
+    uint64_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
     static_assert(H % 16 == 0, "MFMA table needs H multiple of 16");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16;   // 16-neuron row tiles of layer 2
@@ -469,7 +482,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
-    uint32_t map = kIdentityMap, traded = 0;
+    uint64_t map = kIdentityMap;
+    uint32_t traded = 0;
     uint64_t fw = 0;
     // [state][lane] rewards, staged in the activation buffer (the MLP is done
     // with it; the asm is a compiler memory barrier: float and double views of
@@ -480,7 +494,6 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     if (valid) {
         const double mid = tmid, ask = task, bid = tbid, bmax = tbmax, smin = tsmin;
         double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
-        map = 0;
 #pragma unroll
         for (int si = 0; si < NSI; ++si) {
             if (si >= nsi) break;
@@ -489,7 +502,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
             const int32_t ob = act_to_int(rintf(out1[si] * p.act_scale));
             if (!ARL) {
                 const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
-                map |= (uint32_t)(si + so.fill_buy - so.fill_sell) << (3 * si);
+                map = (map & ~(0xFFull << (8 * si))) |
+                      ((uint64_t)(si + so.fill_buy - so.fill_sell) << (8 * si));
                 traded |= (uint32_t)(so.fill_buy | so.fill_sell) << si;
                 rl[si * kWave + lane] = so.reward;
             } else {
@@ -509,13 +523,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
         return;
     }
     SGMM_TSTAMP(wslot, 3, map + traded);
-    uint32_t inc = map;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t before = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc = map_then<(NSI < 8 ? NSI : 8)>(before, inc);
-    }
-    uint32_t excl = __shfl_up(inc, 1, kWave);
+    const uint64_t inc = wave_map_scan(map);
+    uint64_t excl = shfl_up_u64(inc, 1);
     if (lane == 0) excl = kIdentityMap;
     SGMM_TSTAMP(wslot, 4, excl);
     // path planes: plane s holds the reward along the chunk's path from start
@@ -925,7 +934,7 @@ __device__ void generation_tail(const StepArgs& sa, const double* fitness, const
 template <int NSM>
 __global__ __launch_bounds__(kScanThreads) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
-    const uint32_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
+    const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
     const double* __restrict__ rew, double* __restrict__ fitness,
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
@@ -945,20 +954,15 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan(
         int tr = 0;
         for (int c0 = 0; c0 < nch; c0 += kWave) {
             const int c = c0 + lane;
-            const uint32_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
+            const uint64_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
             const uint64_t k = c < nch ? ctr[cb + c] : 0;
-            uint32_t inc = m;
-#pragma unroll
-            for (int d = 1; d < kWave; d <<= 1) {
-                const uint32_t before = __shfl_up(inc, d, kWave);
-                if (lane >= d) inc = map_then<NSM>(before, inc);
-            }
-            uint32_t excl = __shfl_up(inc, 1, kWave);
+            const uint64_t inc = wave_map_scan(m);
+            uint64_t excl = shfl_up_u64(inc, 1);
             if (lane == 0) excl = kIdentityMap;
             const uint32_t st = map_get(excl, s);
             if (c < nch) start[c] = (uint8_t)st;
             tr += (int)((k >> (8 * st)) & 0xFFu);
-            s = map_get(__shfl(inc, kWave - 1, kWave), s);
+            s = map_get(readlane64(inc, kWave - 1), s);
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, kWave);
@@ -1312,12 +1316,12 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 #endif
 
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
-//   no adversary: u32 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
+//   no adversary: u64 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
 //                 slots) | f64 path planes rew[n_states][rs] (rs = total_steps
 //                 rounded up to 32)
 //   adversary:    u64 fills[total_steps] | f64 rew[total_steps][n_states]
 static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
-static size_t ws_cmaps(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint32_t)); }
+static size_t ws_cmaps(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint64_t)); }
 static size_t ws_ctr(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint64_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
@@ -1334,7 +1338,7 @@ template <int H>
 static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
                               const sgmm_ticks& tk, const EpArrays& ep,
                               const sgmm_env_params* params, const GenomeSrc& src, int32_t inv_min,
-                              uint64_t* ctr, uint32_t* cmaps, uint64_t* fills, double* rew) {
+                              uint64_t* ctr, uint64_t* cmaps, uint64_t* fills, double* rew) {
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
 #define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
@@ -1354,7 +1358,7 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
 template <int H>
 static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm_ticks& tk,
                          const EpArrays& ep, const sgmm_env_params* params, const GenomeSrc& src,
-                         int32_t inv_min, uint64_t* ctr, uint32_t* cmaps, uint64_t* fills,
+                         int32_t inv_min, uint64_t* ctr, uint64_t* cmaps, uint64_t* fills,
                          double* rew) {
     const dim3 block(kChunk * nsi);  // one wave per inventory state
 #define SGMM_TABLE(NSM_, ARL_)                                                                  \
@@ -1393,14 +1397,14 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     char* w = reinterpret_cast<char*>(workspace);
     uint64_t* ctr = nullptr;
-    uint32_t* cmaps = nullptr;
+    uint64_t* cmaps = nullptr;
     uint64_t* fills = nullptr;
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
         rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
     } else {
-        cmaps = reinterpret_cast<uint32_t*>(w);
+        cmaps = reinterpret_cast<uint64_t*>(w);
         ctr = reinterpret_cast<uint64_t*>(w + ws_cmaps(eps->n, eps->total_steps));
         rew = reinterpret_cast<double*>(w + ws_cmaps(eps->n, eps->total_steps) +
                                         ws_ctr(eps->n, eps->total_steps));
