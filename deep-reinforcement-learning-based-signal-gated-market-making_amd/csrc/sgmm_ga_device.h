@@ -44,18 +44,34 @@ __device__ __forceinline__ void argmax_merge(double& bv, int& bi, double ov, int
 // np.argmax over one wave (first index on ties, NaN first), lanes with
 // valid: a NaN ballot, a max butterfly, a ballot of the lanes equal to the
 // max.  Returns the winning lane (-1: no valid lane) and its value.
-__device__ __forceinline__ int wave_argmax_first(double f, bool valid, double& bv) {
-    const uint64_t nan = __ballot(valid && f != f);
-    if (nan) {  // wave-uniform
-        bv = __longlong_as_double(0x7FF8000000000000LL);
-        return __ffsll((unsigned long long)nan) - 1;
+__device__ __forceinline__ uint64_t argmax_key(double f) {
+    // order-preserving unsigned key: -0 == +0, NaN above everything
+    if (f != f) return ~0ull;
+    const uint64_t b = (uint64_t)__double_as_longlong(f == 0.0 ? 0.0 : f);
+    return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+
+// wave maximum of an unsigned 64-bit value (DPP row shifts and row
+// broadcasts, integer data only), read from lane 63
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#define SGMM_XSTEP(CTRL, RM)                              \
+    {                                                     \
+        const uint64_t t_ = dpp64<CTRL, RM>(0ull, v);     \
+        v = t_ > v ? t_ : v;                              \
     }
-    double m = valid ? f : -__builtin_inf();
-#pragma unroll
-    for (int off = kWave / 2; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, kWave));
-    const uint64_t hit = __ballot(valid && f == m);
-    bv = m;
-    return hit ? __ffsll((unsigned long long)hit) - 1 : -1;
+    SGMM_XSTEP(0x111, 0xF) SGMM_XSTEP(0x112, 0xF) SGMM_XSTEP(0x114, 0xF)
+    SGMM_XSTEP(0x118, 0xF) SGMM_XSTEP(0x142, 0xA) SGMM_XSTEP(0x143, 0xC)
+#undef SGMM_XSTEP
+    return readlane64(v, kWave - 1);
+}
+
+__device__ __forceinline__ int wave_argmax_first(double f, bool valid, double& bv) {
+    const uint64_t k = valid ? argmax_key(f) : 0ull;
+    const uint64_t m = wave_max_u64(k);
+    const uint64_t hit = __ballot(valid && k == m);
+    const int l = hit ? __ffsll((unsigned long long)hit) - 1 : -1;
+    bv = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(f), l < 0 ? 0 : l));
+    return l;
 }
 
 // np.argmax of fit and of -fit (first index on ties, NaN first) over the
@@ -262,7 +278,9 @@ __device__ __forceinline__ void load_master4(const float* __restrict__ m, int64_
     }
 }
 
-__device__ __forceinline__ void regen_master_regs(float* __restrict__ master, float* lds_master,
+// master <- ask(best) from the registers m; also into best_copy when given
+// (the validation improved: the checkpoint copy, drl_engine.py:133-137)
+__device__ __forceinline__ void regen_master_regs(float* __restrict__ master, float* __restrict__ best_copy,
                                                   int64_t n, const float (&m)[kTailSlots][4],
                                                   float sig, uint64_t seed, uint32_t sid,
                                                   uint32_t gen, int best) {
@@ -277,7 +295,7 @@ __device__ __forceinline__ void regen_master_regs(float* __restrict__ master, fl
             if (4 * k4 + q < n) {
                 const float v = m[j][q] + z[q] * sig;  // ask_row4's arithmetic
                 master[4 * k4 + q] = v;
-                lds_master[4 * k4 + q] = v;
+                if (best_copy) best_copy[4 * k4 + q] = v;
             }
     }
 }
@@ -321,10 +339,10 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
     if (wv < nwa) {
         const int bl = wave_argmax_first(f, mine, bv);
         const int al = wave_argmax_first(-f, mine, av);
-        const int src = bl < 0 ? 0 : bl;
-        pv = __shfl(vf, src, kWave);
-        pt = __shfl(tr, src, kWave);
-        pvt = __shfl(vtr, src, kWave);
+        const int src = bl < 0 ? 0 : bl;  // wave-uniform
+        pv = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(vf), src));
+        pt = __builtin_amdgcn_readlane(tr, src);
+        pvt = __builtin_amdgcn_readlane(vtr, src);
         bi = bl < 0 ? -1 : wv * kWave + bl;
         aj = al < 0 ? -1 : wv * kWave + al;
         // per-wave results: sv[0..nw) best, sv[nw..2nw) its validation fitness, sv[2nw..3nw)
@@ -355,18 +373,18 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
         argmax_merge(av, aj, sv[2 * nw + w], si[3 * nw + w]);
     }
     const int best = bi, abest = aj;
+    // every thread knows whether the validation improved (drl_engine.py:130-131)
+    const int improved = pv > best_val;
     SGMM_TAIL_STAMP(1, best + abest);
-    // ---- tell (model.py:73-76; drl_engine.py:119-125)
-    regen_master_regs(master, lm, n_mm, mm, sig_mm, seed, 0u, gen, best);
-    if (master_adv) regen_master_regs(master_adv, la, n_adv, ma, sig_adv, seed, 1u, gen, abest);
-    SGMM_TAIL_STAMP(2, lm[0]);
-    __syncthreads();  // every wave has read sv/si; lm/la complete
-    SGMM_TAIL_STAMP(3, lm[0]);
+    // ---- tell (model.py:73-76; drl_engine.py:119-125), the checkpoint copy
+    // of the new master written in the same pass
+    regen_master_regs(master, improved ? best_master : nullptr, n_mm, mm, sig_mm, seed, 0u, gen, best);
+    if (master_adv) regen_master_regs(master_adv, nullptr, n_adv, ma, sig_adv, seed, 1u, gen, abest);
+    SGMM_TAIL_STAMP(2, mm[0][0]);
     if (tid == 0) {  // validation of the best (drl_engine.py:129-171)
         const double v = pv, tf = bv;
         double smm = st_smm, sadv = st_sadv;
         int32_t no_improve = no_improve0;
-        const int improved = v > best_val;
         int decayed = 0;
         if (improved) {
             st->best_val = v;
@@ -400,13 +418,10 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
             hist->sigma_after = smm;
             hist->flags = improved | (decayed << 1);
         }
-        si[0] = improved;
     }
-    SGMM_TAIL_STAMP(4, si[0]);
-    __syncthreads();
-    if (si[0] && best_master)
-        for (int64_t k = tid; k < n_mm; k += nt) best_master[k] = lm[k];
-    SGMM_TAIL_STAMP(5, si[0]);
+    SGMM_TAIL_STAMP(4, improved);
+    (void)lm;
+    (void)la;
 }
 
 }  // namespace sgmm

@@ -363,9 +363,6 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
         xs0[q] = tk.s1n[ti];
         xs1[q] = tk.s2n[ti];
     }
-    const int64_t tix = ep.tick_off[e] + min(t0 + lane, T - 1);
-    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
-    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
     // the episode's genomes -> LDS (all four waves, before any of them leaves)
     __shared__ __attribute__((aligned(16))) float gsm[GenomeLayout<H>::N];
     __shared__ float gsa[kAdvParams];
@@ -413,14 +410,14 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     }
     SGMM_TSTAMP(wslot, 1, w2f[0][0] + w1s[KS - 1] + pre[3][KS - 1] + b2c[0][0]);
 
-    // ---- the policy for every (state, tick) of the chunk
+    // ---- the policy for every (state, tick) of the chunk, software-pipelined:
+    // the layer-2 MFMAs of state si+1 are issued beside the layer-3 chains of
+    // state si (which read the activations si left in LDS), then state si+1 is
+    // transposed.  One accumulator set, one activation buffer.
     float out0[NSI], out1[NSI];
-#pragma unroll
-    for (int si = 0; si < NSI; ++si) {
-        out0[si] = out1[si] = 0.0f;
-        if (si >= nsi) continue;
+    f32x4 acc[4][NT];
+    auto layer12 = [&](int si) {  // layer 1 (packed fma) + layer 2 (MFMA) of state si
         const float x2 = (float)((double)(inv_min + si) / 2.0);
-        f32x4 acc[4][NT];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -440,7 +437,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
                     acc[q + 1][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1b, acc[q + 1][rt], 0, 0, 0);
                 }
             }
-        // transpose relu(H2) through LDS: lane n gets tick n's H activations
+    };
+    auto transpose = [&]() {  // relu(H2) through LDS: lane n gets tick n's H activations
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -450,7 +448,15 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
                 for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
                 *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
             }
-        __builtin_amdgcn_wave_barrier();
+    };
+    layer12(0);
+    transpose();
+#pragma unroll
+    for (int si = 0; si < NSI; ++si) {
+        out0[si] = out1[si] = 0.0f;
+        if (si >= nsi) continue;
+        const bool next = si + 1 < nsi;
+        if (next) layer12(si + 1);
         f32x2 o = {g[L::B3], g[L::B3 + 1]};  // both output chains in one packed fma per neuron
 #pragma unroll
         for (int j4 = 0; j4 < H / 4; ++j4) {
@@ -463,8 +469,12 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
         }
         out0[si] = o.x;
         out1[si] = o.y;
-        __builtin_amdgcn_wave_barrier();
+        if (next) transpose();
     }
+    // this lane's tick prices (loaded after the MLP: registers)
+    const int64_t tix = ep.tick_off[e] + min(t0 + lane, T - 1);
+    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
+    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
     SGMM_TSTAMP(wslot, 2, out0[NSI - 1] + out1[0]);
 
     // ---- FPT step from every state, one lane per tick
