@@ -14,16 +14,17 @@
 //     state in parallel.  H >= 16: k_policy_table_mfma, the H x H layer on
 //     v_mfma_f32_16x16x4_f32 (whose k-ordered fused chain IS the canonical
 //     dot-product order); H = 8 or SGMM_TABLE_PATH=valu: k_policy_table, one
-//     lane per (tick, state) on the VALU.  Output per tick: the exclusive
-//     prefix transition map of its 64-tick chunk (+ traded mask) and one
-//     float64 reward per state; per chunk: the chunk's full map.  With the
-//     adversary: 2 fill bits per (inventory, previous fills) state (u64).
+//     lane per (tick, state) on the VALU.  Output: per 64-tick chunk its
+//     transition byte-map and the trade count along the path from each start
+//     state; per tick the path planes (the reward along the chunk's path from
+//     each start state).  With the adversary: 2 fill bits per (inventory,
+//     previous fills) state (u64) and one float64 reward per state.
 //
 //  2. path scan (one workgroup per episode): chunk start states from a scan
-//     of the chunk maps, each tick's state = one field of its prefix word, the
-//     selected rewards summed in the reference's sequential float64 order
-//     (bit-exact), trades counted with a block reduction.  The adversary
-//     variant walks the 20-state transducer chunk by chunk.
+//     of the chunk maps, each tick's reward = one row of its chunk's path
+//     plane, summed in the reference's sequential float64 order (bit-exact,
+//     exact_sum_window), trades from the chunk counts.  The adversary variant
+//     walks the 20-state transducer chunk by chunk.
 //
 // Trace path (sgmm_rollout_trace): k_rollout_direct, one wave per episode,
 // lane = hidden neuron, the literal step loop (independent second
