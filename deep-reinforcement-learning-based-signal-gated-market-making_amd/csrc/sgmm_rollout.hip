@@ -814,45 +814,53 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
 #ifdef SGMM_STAMPS
         unsigned long long n_iter = 0, n_slow = 0;
 #endif
-        // One lane walks (LDS reads return 1/64 of the data of a wave-wide
-        // broadcast read); each iteration is branch-free: the block's reference
-        // additions and the run check run side by side and a select keeps one,
-        // with both possible successors' records already requested.
+        // One lane walks, carrying S as (binade e, integer M) between
+        // fallback blocks: a run jump is integer work only (M += the run's
+        // sum), S is rebuilt as a double just for a fallback block's reference
+        // additions.  Both possible next records (pos + 1 and the run end) are
+        // requested as soon as the current one arrives.
         constexpr int NB = NT / 4;
         if (lane == 0 && nblk > 0) {
             int pos = 0;
+            int e = 0;
+            int64_t M = 0;
+            bool ib = binade_of(S, e, M);  // S = M * 2^(e-52) exactly while ib
             SumRec cur = L.rec[0];
-            do {
+            while (true) {
 #ifdef SGMM_STAMPS
                 ++n_iter;
 #endif
-                const double2* vp = reinterpret_cast<const double2*>(sel + pos * kSumBlk);
-                double2 v[kSumBlk / 2];
-#pragma unroll
-                for (int j = 0; j < kSumBlk / 2; ++j) v[j] = vp[j];
-                const int pn = pos + 1, pj = cur.rend;
-                const SumRec rn = L.rec[min(pn, NB - 1)];
-                const SumRec rj = L.rec[min(pj, NB - 1)];
-                int e;
-                int64_t M;
-                bool ok = binade_of(S, e, M) && cur.be == e;
-                ok = ok && (M > 0 ? (M + cur.mn >= kMLo && M + cur.mx <= kMHi)
-                                  : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi));
-                const double Sj = from_binade(M + cur.dsum, e);
-                double Ss = S;  // the reference way (the last block padded with -0.0)
-#pragma unroll
-                for (int j = 0; j < kSumBlk / 2; ++j) {
-                    Ss += v[j].x;
-                    Ss += v[j].y;
-                }
+                const SumRec rn = L.rec[min(pos + 1, NB - 1)];
+                const SumRec rj = L.rec[min(cur.rend, NB - 1)];
+                const bool ok = ib && cur.be == e &&
+                                (M > 0 ? (M + cur.mn >= kMLo && M + cur.mx <= kMHi)
+                                       : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi));
+                const int64_t Mj = M + cur.dsum;
+                const int pj = cur.rend;
+                if (!ok) {  // this block the reference way (the last block padded with -0.0)
 #ifdef SGMM_STAMPS
-                n_slow += ok ? 0 : 1;
+                    ++n_slow;
 #endif
-                S = ok ? Sj : Ss;
-                pos = ok ? pj : pn;
+                    const double2* vp = reinterpret_cast<const double2*>(sel + pos * kSumBlk);
+                    double2 v[kSumBlk / 2];
+#pragma unroll
+                    for (int j = 0; j < kSumBlk / 2; ++j) v[j] = vp[j];
+                    double s = ib ? from_binade(M, e) : S;
+#pragma unroll
+                    for (int j = 0; j < kSumBlk / 2; ++j) {
+                        s += v[j].x;
+                        s += v[j].y;
+                    }
+                    S = s;
+                    ib = binade_of(s, e, M);
+                }
+                // both successors' records were requested before the decision
+                M = ok ? Mj : M;
+                pos = ok ? pj : pos + 1;
                 cur = ok ? rj : rn;
-            } while (pos < nblk);
-            L.S = S;
+                if (pos >= nblk) break;
+            }
+            L.S = ib ? from_binade(M, e) : S;
         }
 #ifdef SGMM_STAMPS
         if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; }
