@@ -697,15 +697,20 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
     const double sc52 = pow2(52 - (fast ? eb : 0));
     bool bad = !fast;
     int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
+    // rint by the 1.5 * 2^52 shifter: for |q| < 2^51, q + 1.5 * 2^52 lands in
+    // [2^52, 2^53) (ulp 1), so the addition rounds q half-to-even and the
+    // integer is the difference of the bit patterns; a tie is |rint(q) - q| ==
+    // 0.5 (exact: both are multiples of ulp(q) <= 1/4).  Larger steps leave the
+    // binade anyway: the block is flagged.
+    constexpr double kShift = 0x1.8p52;
 #pragma unroll
     for (int j = 0; j < kSumTpt; ++j) {
-        int64_t d = 0;
-        if (fast && i0 + j < n) {
-            const double qv = r[j] * sc52;
-            const bool bj = !(fabs(qv) < 0x1p56) || (qv - floor(qv) == 0.5);
-            bad |= bj;
-            d = bj ? 0 : (int64_t)rint(qv);
-        }
+        const double qv = r[j] * sc52;
+        const double t = qv + kShift;
+        const bool bj = !(fabs(qv) < 0x1p51) || fabs((t - kShift) - qv) == 0.5;
+        const bool use = fast && i0 + j < n;
+        bad |= use && bj;
+        const int64_t d = (use && !bj) ? __double_as_longlong(t) - __double_as_longlong(kShift) : 0;
         P += d;
         mn = min(mn, P);
         mx = max(mx, P);
