@@ -667,115 +667,104 @@ struct SumLds {
 // with a barrier (sel may then be refilled).
 template <int NT>
 __device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L) {
-    static_assert(NT % kWave == 0 && NT / 4 <= (1 << 30), "whole waves");
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6, qd = lane & 3, q = lane >> 2;
-    const int i0 = tid * kSumTpt;
-    double r[kSumTpt];
+    static_assert(NT % (4 * kWave) == 0, "whole block waves");
+    constexpr int NB = NT / 4;         // 16-value blocks per window
+    constexpr int NWB = NB / kWave;    // waves holding one block per lane
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
+    const int b = tid;                 // this lane's block (waves < NWB)
+    const int i0 = b * kSumBlk;
+    const bool blk = wv < NWB;         // wave-uniform
+    const bool live = blk && i0 < n;
+    double r[kSumBlk];
+    float fex = 0.0f;
+    if (blk) {
+        // the block's values; the last block padded with -0.0 in LDS (x + -0.0
+        // == x for every x, -0.0 and NaN included), so a fallback block always
+        // adds 16 values
 #pragma unroll
-    for (int j = 0; j < kSumTpt; ++j) r[j] = i0 + j < n ? sel[i0 + j] : 0.0;
-    // the last block padded with -0.0 (x + -0.0 == x for every x, -0.0 and NaN
-    // included), so a fallback block always adds 16 values
-    if (i0 < ((n + kSumBlk - 1) & ~(kSumBlk - 1)))
+        for (int j = 0; j < kSumBlk; j += 2) {
+            const double2 v = live ? *reinterpret_cast<const double2*>(sel + i0 + j) : double2{0.0, 0.0};
+            r[j] = i0 + j < n ? v.x : 0.0;
+            r[j + 1] = i0 + j + 1 < n ? v.y : 0.0;
+        }
+        if (live && i0 + kSumBlk > n)
+            for (int j = n - i0; j < kSumBlk; ++j) const_cast<double*>(sel)[i0 + j] = -0.0;
+        // a. approximate block starts (binade predictions only: float32 is enough)
+        double a = 0.0;
 #pragma unroll
-        for (int j = 0; j < kSumTpt; ++j)
-            if (i0 + j >= n) const_cast<double*>(sel)[i0 + j] = -0.0;
-    // a. approximate block starts (binade predictions only: float32 is enough)
-    const float fv = (float)(((r[0] + r[1]) + r[2]) + r[3]);
-    const float finc = wave_scan_add_f32(fv);
-    const float fbs = __int_as_float((int)dpp32<0x00>(0u, (uint32_t)__float_as_int(finc - fv)));
-    if (lane == kWave - 1) L.w_ap[wv] = finc;
+        for (int j = 0; j < kSumBlk; ++j) a += r[j];
+        const float fv = (float)a;
+        const float finc = wave_scan_add_f32(fv);
+        fex = finc - fv;
+        if (lane == kWave - 1) L.w_ap[wv] = finc;
+    }
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 8);
-    float woff = 0.0f;  // the preceding waves' totals (broadcast reads, in order)
+    if (blk) {
+        float woff = 0.0f;  // the preceding block waves' totals (broadcast reads, in order)
 #pragma unroll
-    for (int k = 0; k < NT / kWave; ++k) woff += k < wv ? L.w_ap[k] : 0.0f;
-    // b. integer steps of the block in its predicted binade
-    const bool blive = (tid & ~3) * kSumTpt < n;  // the block has values (uniform per quad)
-    int eb = 0;
-    int64_t ma = 0;  // the approximate start's mantissa
-    const bool fast = blive && binade_of(S + (double)(woff + fbs), eb, ma);
-    const double sc52 = pow2(52 - (fast ? eb : 0));
-    bool bad = !fast;
-    int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
-    // rint by the 1.5 * 2^52 shifter: for |q| < 2^51, q + 1.5 * 2^52 lands in
-    // [2^52, 2^53) (ulp 1), so the addition rounds q half-to-even and the
-    // integer is the difference of the bit patterns; a tie is |rint(q) - q| ==
-    // 0.5 (exact: both are multiples of ulp(q) <= 1/4).  Larger steps leave the
-    // binade anyway: the block is flagged.
-    constexpr double kShift = 0x1.8p52;
+        for (int k = 0; k < NWB; ++k) woff += k < wv ? L.w_ap[k] : 0.0f;
+        // b. integer steps of the block in its predicted binade
+        int eb = 0;
+        int64_t ma = 0;  // the approximate start's mantissa
+        const bool fast = live && binade_of(S + (double)(woff + fex), eb, ma);
+        const double sc52 = pow2(52 - (fast ? eb : 0));
+        bool bad = !fast;
+        int64_t P = 0, mn = INT64_MAX, mx = INT64_MIN;
+        // rint by the 1.5 * 2^52 shifter: for |q| < 2^51, q + 1.5 * 2^52 lands
+        // in [2^52, 2^53) (ulp 1), so the addition rounds q half-to-even and the
+        // integer is the difference of the bit patterns; a tie is |rint(q) - q|
+        // == 0.5 (exact: both are multiples of ulp(q) <= 1/4).  Larger steps
+        // leave the binade anyway: the block is flagged.
+        constexpr double kShift = 0x1.8p52;
 #pragma unroll
-    for (int j = 0; j < kSumTpt; ++j) {
-        const double qv = r[j] * sc52;
-        const double t = qv + kShift;
-        const bool bj = !(fabs(qv) < 0x1p51) || fabs((t - kShift) - qv) == 0.5;
-        const bool use = fast && i0 + j < n;
-        bad |= use && bj;
-        const int64_t d = (use && !bj) ? __double_as_longlong(t) - __double_as_longlong(kShift) : 0;
-        P += d;
-        mn = min(mn, P);
-        mx = max(mx, P);
-    }
-    // inclusive prefix of the lane totals over the quad (the DPP moves run in
-    // every lane: a move whose source lane is inactive returns 0)
-    uint64_t qinc = (uint64_t)P;
-    {
-        const uint64_t t1 = dpp64<0x111>(0, qinc);
-        qinc += qd >= 1 ? t1 : 0;
-        const uint64_t t2 = dpp64<0x112>(0, qinc);
-        qinc += qd >= 2 ? t2 : 0;
-    }
-    const int64_t ex = (int64_t)(qinc - (uint64_t)P);
-    int64_t qmn = mn + ex, qmx = mx + ex;
-    {
-        int64_t t = (int64_t)dpp64<0x111>((uint64_t)INT64_MAX, (uint64_t)qmn);
-        qmn = min(qmn, qd >= 1 ? t : INT64_MAX);
-        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MAX, (uint64_t)qmn);
-        qmn = min(qmn, qd >= 2 ? t : INT64_MAX);
-        t = (int64_t)dpp64<0x111>((uint64_t)INT64_MIN, (uint64_t)qmx);
-        qmx = max(qmx, qd >= 1 ? t : INT64_MIN);
-        t = (int64_t)dpp64<0x112>((uint64_t)INT64_MIN, (uint64_t)qmx);
-        qmx = max(qmx, qd >= 2 ? t : INT64_MIN);
-    }
-    // a block whose predicted prefix comes within 2^-12 of the binade's edges
-    // (the float32 start's error is far below that) most likely crosses it:
-    // no prediction, so the runs before it stay fast and it is added the
-    // reference way
-    const bool edge = qd == 3 && fast &&
-                      (ma > 0 ? (ma + qmx > kMHi - kEdge || ma + qmn < kMLo + kEdge)
-                              : (ma + qmn < -kMHi + kEdge || ma + qmx > -kMLo - kEdge));
-    const uint64_t bl = __ballot(bad || edge);
-    const int32_t be = (fast && ((bl >> (lane & ~3)) & 0xFu) == 0) ? eb : INT32_MIN;
-    // block sums at the quad leaders (qd == 3) -> wave-local exclusive prefix zl
-    const uint64_t bt = qd == 3 ? qinc : 0;
-    const uint64_t zinc = wave_scan_add(bt);
-    const int64_t zl = (int64_t)(zinc - bt);
-    const int64_t wtot = (int64_t)readlane64(zinc, kWave - 1);
-    // runs inside the wave: a leader starts a run when its prediction differs
-    // from the previous block's
-    const int32_t bprev = __shfl_up(be, 4, kWave);
-    const uint64_t starts = __ballot(qd == 3 && (q == 0 || be != bprev));
-    const uint64_t later = lane == kWave - 1 ? 0ull : starts & (~0ull << (lane + 1));
-    const int rq = later ? (__ffsll((unsigned long long)later) - 1) >> 2 : kWave / 4;
-    // segmented suffix min / max of the in-wave prefix extremes over [q, rq)
-    int64_t amn = zl + qmn, amx = zl + qmx;
-#pragma unroll
-    for (int d = 1; d < kWave / 4; d <<= 1) {
-        const int64_t omn = shfl_i64(amn, min(lane + 4 * d, kWave - 1));
-        const int64_t omx = shfl_i64(amx, min(lane + 4 * d, kWave - 1));
-        if (q + d < rq) {
-            amn = min(amn, omn);
-            amx = max(amx, omx);
+        for (int j = 0; j < kSumBlk; ++j) {
+            const double qv = r[j] * sc52;
+            const double t = qv + kShift;
+            const bool bj = !(fabs(qv) < 0x1p51) || fabs((t - kShift) - qv) == 0.5;
+            const bool use = fast && i0 + j < n;
+            bad |= use && bj;
+            const int64_t d = (use && !bj) ? __double_as_longlong(t) - __double_as_longlong(kShift) : 0;
+            P += d;
+            mn = min(mn, P);
+            mx = max(mx, P);
         }
-    }
-    const int64_t zr = shfl_i64(zl, 4 * min(rq, kWave / 4 - 1) + 3);
-    if (qd == 3) {
+        // a block whose predicted prefix comes within 2^-12 of the binade's
+        // edges (the float32 start's error is far below that) most likely
+        // crosses it: no prediction, so the runs before it stay fast and it is
+        // added the reference way
+        const bool edge = fast && (ma > 0 ? (ma + mx > kMHi - kEdge || ma + mn < kMLo + kEdge)
+                                          : (ma + mn < -kMHi + kEdge || ma + mx > -kMLo - kEdge));
+        const int32_t be = (fast && !bad && !edge) ? eb : INT32_MIN;
+        // block sums -> wave-local exclusive prefix zl
+        const uint64_t zinc = wave_scan_add((uint64_t)P);
+        const int64_t zl = (int64_t)(zinc - (uint64_t)P);
+        const int64_t wtot = (int64_t)readlane64(zinc, kWave - 1);
+        // runs inside the wave: a block starts a run when its prediction
+        // differs from the previous block's
+        const int32_t bprev = __shfl_up(be, 1, kWave);
+        const uint64_t starts = __ballot(lane == 0 || be != bprev);
+        const uint64_t later = lane == kWave - 1 ? 0ull : starts & (~0ull << (lane + 1));
+        const int rq = later ? __ffsll((unsigned long long)later) - 1 : kWave;
+        // segmented suffix min / max of the in-wave prefix extremes over [lane, rq)
+        int64_t amn = zl + mn, amx = zl + mx;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            const int64_t omn = shfl_i64(amn, min(lane + d, kWave - 1));
+            const int64_t omx = shfl_i64(amx, min(lane + d, kWave - 1));
+            if (lane + d < rq) {
+                amn = min(amn, omn);
+                amx = max(amx, omx);
+            }
+        }
+        const int64_t zr = shfl_i64(zl, min(rq, kWave - 1));
         SumRec rc;
         rc.mn = amn - zl;
         rc.mx = amx - zl;
-        rc.dsum = (rq < kWave / 4 ? zr : wtot) - zl;
+        rc.dsum = (rq < kWave ? zr : wtot) - zl;
         rc.be = be;
-        rc.rend = wv * (kWave / 4) + rq;
-        L.rec[wv * (kWave / 4) + q] = rc;
+        rc.rend = wv * kWave + rq;
+        L.rec[b] = rc;
     }
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 9);
@@ -786,11 +775,11 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
         // wave's first block) is extended over the following waves while each
         // is one run with the same prediction -- a segmented suffix scan of
         // (min, max, sum) over the heads, lanes w < NT/64
-        constexpr int NW = NT / kWave;
+        constexpr int NW = NT / (4 * kWave);  // block waves
         if (lane < NW) {
-            const SumRec h = L.rec[lane * (kWave / 4)];
+            const SumRec h = L.rec[lane * kWave];
             const int32_t bnext = __shfl_down(h.be, 1, kWave);
-            const bool link = lane + 1 < NW && h.rend == (lane + 1) * (kWave / 4) && bnext == h.be;
+            const bool link = lane + 1 < NW && h.rend == (lane + 1) * kWave && bnext == h.be;
             const uint64_t brk = __ballot(!link) & ((1ull << NW) - 1);
             const uint64_t atl = brk & (~0ull << lane);  // the first break at or after this wave
             const int k = __ffsll((unsigned long long)atl) - 1;
@@ -808,7 +797,7 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                     re = ore;
                 }
             }
-            SumRec& hw = L.rec[lane * (kWave / 4)];
+            SumRec& hw = L.rec[lane * kWave];
             hw.mn = mn;
             hw.mx = mx;
             hw.dsum = ds;
