@@ -570,31 +570,33 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
 // long as the exact S + r stays inside the binade and r/u is not a tie (x.5).
 // So a stretch of ticks that keeps one binade adds up as 64-bit integers.
 //
-// A window of 4 NT values (NT threads, 4 consecutive values each, a 16-value
-// block = one quad of lanes):
+// A window of 4 NT values, cut into NT/4 blocks of 16 values, one block per
+// lane of the first NT/256 waves:
 //   a. float32 approximate block starts (wave scan + the waves' totals);
 //   b. per block: the binade predicted from its approximate start, its integer
 //      steps d = rint(r/u), their prefix range and a flag for ties / huge
-//      steps.  Blocks of one wave that share a predicted binade form a run;
-//      every block gets the record of the rest of its run (segmented suffix
-//      min / max of the integer prefixes, the run's integer sum, its end);
-//   c. one wave walks the blocks from the exact S with scalar control flow:
-//      if S's binade is the block's prediction and M plus the run's prefix
-//      range stays strictly inside [2^52, 2^53), the whole rest of the run is
-//      added as one integer; otherwise the block is added with the reference's
-//      float64 additions (its values are already in registers) and the walk
-//      moves to the next block.
+//      steps / a predicted range near the binade's edges.  Blocks of one wave
+//      that share a predicted binade form a run; every block gets the record
+//      of the rest of its run (segmented suffix min / max of the integer
+//      prefixes, the run's integer sum, its end); wave 0 extends each wave's
+//      head record over the following waves;
+//   c. one lane walks the blocks from the exact S, kept as (binade, integer
+//      M) between fallback blocks: if S's binade is the block's prediction
+//      and M plus the run's prefix range stays strictly inside [2^52, 2^53),
+//      the whole rest of the run is added as one integer; otherwise the block
+//      is added with the reference's float64 additions and the walk moves to
+//      the next block.
 // Every accepted shortcut is exact by the property above, so the result is
 // the sequential sum bit for bit.  On a bench episode the walk takes ~10
 // fallback blocks (the sum's doublings: ticks 2, 3, 6, 16, 22, 43, 85, ...)
-// and a few run jumps per 256-value wave.
+// and ~11 run jumps.
 constexpr int kSumBlk = 16;
-constexpr int kSumTpt = 4;          // values per thread
+constexpr int kSumTpt = 4;          // rewards gathered per path-scan thread
 constexpr int kScanThreads = 1024;  // path-scan workgroup
 constexpr int kScanWin = kScanThreads * kSumTpt;
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
-static_assert(kSumBlk == 4 * kSumTpt, "a block is one quad of lanes");
+static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
 
 // S = M * 2^(e-52) with |M| in [2^52, 2^53); false unless S is normal with
 // |e| <= 900 (the shortcut's range: 2^(52-e) and its inverse stay normal)
