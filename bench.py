@@ -177,9 +177,10 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = world * P * T * args.steps / dt
 
-    # per-kernel durations: eager generations of the same workload bracketed by
-    # HIP events on the launch stream (sgmm_profile_*); graph replays launch the
-    # identical kernels
+    # per-kernel durations: eager generations of the same workload; the library
+    # hands each profiled kernel a pair of HIP events recorded by its own dispatch
+    # on the launch stream (hipExtLaunchKernel, sgmm_profile_*); graph replays
+    # launch the identical kernels
     peng = sgmm.DRLEngine(pop_size=P, phi=args.phi, tick_size=0.001, use_arl=False, save_dir=tmp,
                           hidden_dim=H, rng="device", seed=99, val_mode="fused", sync_every=10**9,
                           verbose=False, use_graph=False, dist=False)

@@ -19,6 +19,8 @@ std::mutex g_prof_mu;
 bool g_prof_on = false;
 std::vector<ProfRec> g_prof;
 std::vector<hipEvent_t> g_event_pool;
+thread_local int g_open_slot = -1;  // slot of this thread's innermost open scope
+thread_local bool g_open_taken = false;
 
 hipEvent_t take_event() {
     if (!g_event_pool.empty()) {
@@ -48,11 +50,26 @@ int prof_begin(const char* kind, hipStream_t s) {
     if (!r.a || !r.b) return -1;
     (void)hipEventRecord(r.a, s);
     g_prof.push_back(r);
-    return (int)g_prof.size() - 1;
+    g_open_slot = (int)g_prof.size() - 1;
+    g_open_taken = false;
+    return g_open_slot;
+}
+
+bool prof_take_events(hipEvent_t* start, hipEvent_t* stop) {
+    if (g_open_slot < 0 || g_open_taken) return false;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    if (g_open_slot >= (int)g_prof.size()) return false;
+    *start = g_prof[g_open_slot].a;
+    *stop = g_prof[g_open_slot].b;
+    g_open_taken = true;
+    return true;
 }
 
 void prof_end(int slot, hipStream_t s) {
     if (slot < 0) return;
+    const bool taken = slot == g_open_slot && g_open_taken;
+    if (slot == g_open_slot) g_open_slot = -1;
+    if (taken) return;  // the kernel's dispatch records both events
     std::lock_guard<std::mutex> lk(g_prof_mu);
     if (slot < (int)g_prof.size()) (void)hipEventRecord(g_prof[slot].b, s);
 }

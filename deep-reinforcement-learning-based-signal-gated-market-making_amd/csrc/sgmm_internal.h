@@ -1,6 +1,7 @@
 // sgmm_internal.h -- host-side helpers shared by the C-ABI translation units.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
@@ -44,8 +45,21 @@ inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s);
 
 // Kernel-timing hooks (sgmm_profile_enable).  prof_begin returns a slot
 // (or -1 when profiling is off) that prof_end closes on the same stream.
+// A kernel launched inside the scope with SGMM_LAUNCH takes the slot's events
+// into its own dispatch (hipExtLaunchKernel), so the slot then times the kernel
+// itself rather than the span between two stream markers.
 int prof_begin(const char* kind, hipStream_t s);
 void prof_end(int slot, hipStream_t s);
+bool prof_take_events(hipEvent_t* start, hipEvent_t* stop);
+
+#define SGMM_LAUNCH(kernel, grid, block, lds, stream, ...)                                       \
+    do {                                                                                         \
+        hipEvent_t ev_a_, ev_b_;                                                                 \
+        if (::sgmm::prof_take_events(&ev_a_, &ev_b_))                                            \
+            hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, ev_a_, ev_b_, 0, __VA_ARGS__); \
+        else                                                                                     \
+            hipLaunchKernelGGL(kernel, grid, block, lds, stream, __VA_ARGS__);                   \
+    } while (0)
 
 struct ProfScope {
     int slot;

@@ -1357,7 +1357,7 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
 #define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
-    hipLaunchKernelGGL((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
+    SGMM_LAUNCH((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
                        src, inv_min, nsi, ctr, cmaps, fills, rew)
     if (arl) {
         if (nsi <= 5) SGMM_TABLE_MFMA(5, true);
@@ -1377,7 +1377,7 @@ static void launch_table(bool arl, int nsi, dim3 grid, hipStream_t s, const sgmm
                          double* rew) {
     const dim3 block(kChunk * nsi);  // one wave per inventory state
 #define SGMM_TABLE(NSM_, ARL_)                                                                  \
-    hipLaunchKernelGGL((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, src, \
+    SGMM_LAUNCH((k_policy_table<H, NSM_, ARL_>), grid, block, 0, s, tk, ep, params, src, \
                        inv_min, nsi, ctr, cmaps, fills, rew)
     if (arl) SGMM_TABLE(8, true);
     else if (nsi <= 5) SGMM_TABLE(5, false);
@@ -1390,7 +1390,7 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
     clear_error();
     SGMM_REQUIRE(out && (values || n == 0) && n >= 0, "bad arguments");
     ProfScope prof("ordered_sum", as_stream(stream));
-    hipLaunchKernelGGL(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
+    SGMM_LAUNCH(k_ordered_sum, dim3(1), dim3(kScanThreads), 0, as_stream(stream), values, n,
                        init, out);
     SGMM_LAUNCHED();
     return SGMM_OK;
@@ -1451,16 +1451,16 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     if (arl) {
         size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanBlock, step));
-        hipLaunchKernelGGL(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
+        SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
         size_t lds = kScanWin * sizeof(double);
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
         if (nsi <= 5)
-            hipLaunchKernelGGL(k_path_scan<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
+            SGMM_LAUNCH(k_path_scan<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
                                eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
         else
-            hipLaunchKernelGGL(k_path_scan<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
+            SGMM_LAUNCH(k_path_scan<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
                                eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
     }
     SGMM_LAUNCHED();
@@ -1539,10 +1539,10 @@ extern "C" int sgmm_rollout_trace(const sgmm_ticks* ticks, const sgmm_episodes* 
     hipStream_t s = as_stream(stream);
     ProfScope prof("rollout_direct", s);
     switch (hidden) {
-        case 8: hipLaunchKernelGGL(k_rollout_direct<8>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
-        case 16: hipLaunchKernelGGL(k_rollout_direct<16>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
-        case 32: hipLaunchKernelGGL(k_rollout_direct<32>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
-        default: hipLaunchKernelGGL(k_rollout_direct<64>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
+        case 8: SGMM_LAUNCH(k_rollout_direct<8>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
+        case 16: SGMM_LAUNCH(k_rollout_direct<16>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
+        case 32: SGMM_LAUNCH(k_rollout_direct<32>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
+        default: SGMM_LAUNCH(k_rollout_direct<64>, dim3(eps->n), dim3(kWave), 0, s, *ticks, ep, params, mm_genomes, mm_stride, adv_genomes, adv_stride, eps->inv_min, nsi, o); break;
     }
     SGMM_LAUNCHED();
     return SGMM_OK;
@@ -1561,10 +1561,10 @@ extern "C" int sgmm_policy_forward(const float* genomes, int64_t genome_stride, 
     hipStream_t s = as_stream(stream);
     ProfScope prof("policy_forward", s);
     switch (hidden) {
-        case 8: hipLaunchKernelGGL(k_policy_forward<8>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
-        case 16: hipLaunchKernelGGL(k_policy_forward<16>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
-        case 32: hipLaunchKernelGGL(k_policy_forward<32>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
-        default: hipLaunchKernelGGL(k_policy_forward<64>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
+        case 8: SGMM_LAUNCH(k_policy_forward<8>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
+        case 16: SGMM_LAUNCH(k_policy_forward<16>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
+        case 32: SGMM_LAUNCH(k_policy_forward<32>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
+        default: SGMM_LAUNCH(k_policy_forward<64>, grid, blk, 0, s, genomes, genome_stride, genome_idx, states, out, n); break;
     }
     SGMM_LAUNCHED();
     return SGMM_OK;
@@ -1578,7 +1578,7 @@ extern "C" int sgmm_adversary_forward(const float* genomes, int64_t genome_strid
     SGMM_REQUIRE(n >= 0 && genome_stride >= 74, "bad n or stride");
     if (n == 0) return SGMM_OK;
     ProfScope prof("adversary_forward", as_stream(stream));
-    hipLaunchKernelGGL(k_adversary_forward, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+    SGMM_LAUNCH(k_adversary_forward, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        as_stream(stream), genomes, genome_stride, genome_idx, states, out, n);
     SGMM_LAUNCHED();
     return SGMM_OK;
@@ -1599,7 +1599,7 @@ extern "C" int sgmm_env_step_batch(const sgmm_env_params* params, const int32_t*
     SGMM_REQUIRE(n >= 0, "n < 0");
     if (n == 0) return SGMM_OK;
     ProfScope prof("env_step", as_stream(stream));
-    hipLaunchKernelGGL(k_env_step, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+    SGMM_LAUNCH(k_env_step, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        as_stream(stream), params, param_idx, inventory, cash, action, adv_action,
                        mid_next, best_ask, best_bid, buy_max, sell_min, reward, pnl_reward,
                        inventory_reward, fee_paid, fill_buy, fill_sell, n);
