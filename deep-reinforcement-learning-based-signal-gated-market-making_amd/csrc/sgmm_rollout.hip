@@ -285,6 +285,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
 // s_memrealtime at entry (a clock common to all XCDs)
 __device__ unsigned long long g_stamps[4096][16];
 __device__ unsigned long long g_tstamps[8192][8];
+__device__ unsigned int g_thwid[8192][2];  // HW_ID, XCC_ID of each table wave
 #define SGMM_STAMP(e, k)                                                           \
     do {                                                                           \
         unsigned long long t_;                                                     \
@@ -303,6 +304,10 @@ __device__ unsigned long long g_tstamps[8192][8];
         unsigned long long t_;                                                         \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
         if ((threadIdx.x & 63) == 0 && (w) < 8192) g_tstamps[w][k] = t_;               \
+        unsigned h_, x_;                                                               \
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" \
+                     : "=s"(h_), "=s"(x_));                                            \
+        if ((threadIdx.x & 63) == 0 && (w) < 8192) { g_thwid[w][0] = h_; g_thwid[w][1] = x_; } \
     } while (0)
 #else
 #define SGMM_STAMP(e, k) \
@@ -1324,6 +1329,9 @@ extern "C" int sgmm_debug_stamps(unsigned long long* host, int n_eps) {
 }
 extern "C" int sgmm_debug_tail(unsigned long long* host) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tail), sizeof(unsigned long long) * 8);
+}
+extern "C" int sgmm_debug_thwid(unsigned int* host, int n_waves) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_thwid), sizeof(unsigned int) * 2 * n_waves);
 }
 extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * n_waves);
