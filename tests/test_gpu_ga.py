@@ -171,6 +171,32 @@ def test_device_rng_modes_agree(sgmm, tmp_path, arl):
     assert s0 < 0.05  # patience 4 over 25 generations decays sigma at least once
 
 
+def test_device_modes_agree_with_nan_fitness(sgmm, tmp_path):
+    """NaN training fitness (a NaN mid_next at ticks where only some
+    individuals' quotes fill) follows np.argmax -- the first NaN wins -- in the
+    fused in-scan GA step exactly as in the separate tell/val launches."""
+    tr, va, st = _bundles(5)
+    s1, s2, mid, ask, bid, bmax, smin = (a.copy() for a in tr)
+    for j, t in enumerate(range(40, 600, 70)):
+        mid[t] = np.nan
+        smin[t] = np.nan                      # no buy fill at t
+        bmax[t] = ask[t] + (j % 3 - 1) * 0.001  # a sell fill only for some offsets
+    tr = (s1, s2, mid, ask, bid, bmax, smin)
+    res = []
+    for use_graph, val_mode in ((True, "fused"), (False, "best")):
+        torch.manual_seed(3)
+        eng = sgmm.DRLEngine(pop_size=24, sigma=0.2, phi=0.0005, tick_size=0.001, save_dir=str(tmp_path / val_mode),
+                             hidden_dim=16, rng="device", seed=7, val_mode=val_mode, use_graph=use_graph,
+                             verbose=False, sync_every=5, patience=4)
+        pol, hist = eng.train(tr, va, st, generations=12)
+        res.append((hist, pol.get_weights().numpy(), eng.mm_evolver.sigma))
+    (h0, w0, s0), (h1, w1, s1_) = res
+    assert np.isnan(np.array(h0["train_f"], np.float64)).any()  # the NaN path is exercised
+    for k in h0:
+        assert np.array_equal(np.array(h1[k], np.float64), np.array(h0[k], np.float64), equal_nan=True), k
+    assert np.array_equal(w0, w1) and s0 == s1_
+
+
 def test_device_ga_fitness_matches_reevaluation(sgmm, tmp_path):
     """history['train_f'] of each generation equals re-evaluating the master it
     produced, and the returned policy re-evaluates to the best validation reward."""
