@@ -599,6 +599,8 @@ constexpr int kSumBlk = 16;
 constexpr int kSumTpt = 4;          // rewards gathered per path-scan thread
 constexpr int kScanThreads = 1024;  // path-scan workgroup
 constexpr int kScanWin = kScanThreads * kSumTpt;
+constexpr int kScanSmall = 256;      // path-scan workgroup when there are many episodes:
+constexpr int kScanManyAbove = 512;  // more than two 16-wave workgroups per CU
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
 static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
@@ -951,15 +953,16 @@ __device__ void generation_tail(const StepArgs& sa, const double* fitness, const
 //   2. every thread: the rewards of its 4 ticks from the path plane of their
 //      chunk's start state (one coalesced row per chunk) -> LDS;
 //   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
-template <int NSM>
-__global__ __launch_bounds__(kScanThreads) void k_path_scan(
+template <int NSM, int NT>
+__global__ __launch_bounds__(NT) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
     const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
     const double* __restrict__ rew, double* __restrict__ fitness,
     int32_t* __restrict__ trades_out, StepArgs step) {
+    constexpr int kWin = NT * kSumTpt;
     extern __shared__ __align__(16) unsigned char lds[];
-    double* sel = reinterpret_cast<double*>(lds);  // [kScanWin]
-    __shared__ SumLds<kScanThreads> L;
+    double* sel = reinterpret_cast<double*>(lds);  // [kWin]
+    __shared__ SumLds<NT> L;
     __shared__ uint8_t start[kMaxLen / kChunk];
     __shared__ int red_trades;
     const int e = blockIdx.x;
@@ -991,8 +994,8 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan(
     __syncthreads();
     SGMM_STAMP(e, 1);
     double S = 0.0;  // exact running sum (identical in every thread between windows)
-    for (int w0 = 0; w0 < T; w0 += kScanWin) {
-        const int n = min(kScanWin, T - w0);
+    for (int w0 = 0; w0 < T; w0 += kWin) {
+        const int n = min(kWin, T - w0);
         const int i0 = tid * kSumTpt;
         if (i0 < n) {  // 4 ticks of one chunk (kChunk % kSumTpt == 0)
             const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
@@ -1005,7 +1008,7 @@ __global__ __launch_bounds__(kScanThreads) void k_path_scan(
         }
         __syncthreads();
         SGMM_STAMP(e, 2);
-        S = exact_sum_window<kScanThreads>(sel, n, S, L);
+        S = exact_sum_window<NT>(sel, n, S, L);
     }
     SGMM_STAMP(e, 3);
     if (tid == 0) {
@@ -1462,14 +1465,26 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
-        size_t lds = kScanWin * sizeof(double);
-        if (step.st) lds = std::max(lds, step_lds_bytes(kScanThreads, step));
-        if (nsi <= 5)
-            SGMM_LAUNCH(k_path_scan<5>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
-                               eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+        // a few episodes: one 16-wave workgroup each (4096-tick windows, the
+        // phases spread over the whole CU); many episodes: 4-wave workgroups
+        // (1024-tick windows), up to eight resident per CU, so the serial
+        // walks of different episodes overlap instead of idling the CU
+        const bool many = eps->n > kScanManyAbove;
+        const int nt = many ? kScanSmall : kScanThreads;
+        size_t lds = (size_t)nt * kSumTpt * sizeof(double);
+        if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
+        if (nsi <= 5 && many)
+            SGMM_LAUNCH((k_path_scan<5, kScanSmall>), dim3(eps->n), dim3(nt), lds, s, ep, params,
+                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+        else if (nsi <= 5)
+            SGMM_LAUNCH((k_path_scan<5, kScanThreads>), dim3(eps->n), dim3(nt), lds, s, ep, params,
+                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+        else if (many)
+            SGMM_LAUNCH((k_path_scan<8, kScanSmall>), dim3(eps->n), dim3(nt), lds, s, ep, params,
+                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
         else
-            SGMM_LAUNCH(k_path_scan<8>, dim3(eps->n), dim3(kScanThreads), lds, s, ep, params,
-                               eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+            SGMM_LAUNCH((k_path_scan<8, kScanThreads>), dim3(eps->n), dim3(nt), lds, s, ep, params,
+                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
     }
     SGMM_LAUNCHED();
     return SGMM_OK;

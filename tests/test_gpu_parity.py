@@ -205,6 +205,31 @@ def test_bench_config_population(sgmm, oracle):
     assert np.array_equal(fit, want_f)
 
 
+def test_many_episode_scan(sgmm, oracle):
+    """More than 512 episodes take the 4-wave path scan (1024-tick windows):
+    ragged lengths around its window boundaries, every episode bit-exact."""
+    from sgmm_amd import synthetic
+    T, H = 5000, 16
+    base = [0, 1, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3600, 4096, 5000]
+    lens = np.array([base[i % len(base)] if i < 96 else 700 + (37 * i) % 4300 for i in range(600)], np.int64)
+    P = len(lens)
+    b = synthetic.bundle_510300(T, seed=3)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=0.2, seed=4)
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0001, tick_size=0.001)], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P)).to(DEV)
+    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,
+                                           np.zeros(P), lens, np.zeros(P),
+                                           [oracle.params(phi=0.0001, tick=0.001)], n_threads=8)
+    assert np.array_equal(trd.cpu().numpy(), want_t)
+    assert np.array_equal(fit.cpu().numpy(), want_f)
+
+
 def test_inventory_range_variants(sgmm, oracle):
     """Non-default caps (i_max=1, i_min=-3): 5 states, 0 not centred."""
     eps = _synthetic_batch(sgmm, 4, 700, 16, seed=31, sigma=0.5)
