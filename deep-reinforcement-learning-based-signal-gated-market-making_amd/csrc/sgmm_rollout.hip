@@ -599,8 +599,8 @@ constexpr int kSumBlk = 16;
 constexpr int kSumTpt = 4;          // rewards gathered per path-scan thread
 constexpr int kScanThreads = 1024;  // path-scan workgroup
 constexpr int kScanWin = kScanThreads * kSumTpt;
-constexpr int kScanSmall = 256;      // path-scan workgroup when there are many episodes:
-constexpr int kScanManyAbove = 512;  // more than two 16-wave workgroups per CU
+constexpr int kScanAt1024 = 256;  // path-scan workgroup: 1024 threads up to this many episodes,
+constexpr int kScanAt512 = 1024;  // 512 up to this many, 256 above
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
 static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
@@ -1407,6 +1407,28 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
     return SGMM_OK;
 }
 
+// path-scan workgroup size for n episodes (256 CUs): one 16-wave workgroup per
+// CU while they fit, then 8-wave, then 4-wave workgroups
+static int scan_threads(int64_t n) {
+    return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : 256);
+}
+
+template <int NSM>
+static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
+                             const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
+                             const uint64_t* ctr, const double* rew, double* fitness, int32_t* trades,
+                             const StepArgs& step) {
+    if (nt == kScanThreads)
+        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, rew, fitness, trades, step);
+    else if (nt == 512)
+        SGMM_LAUNCH((k_path_scan<NSM, 512>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    rew, fitness, trades, step);
+    else
+        SGMM_LAUNCH((k_path_scan<NSM, 256>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    rew, fitness, trades, step);
+}
+
 // table + path scan (+ the generation tail when step.st) for one batch
 static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                         const sgmm_env_params* params, const GenomeSrc& src, bool arl,
@@ -1465,26 +1487,20 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
                            eps->inv_min, nsi, fills, rew, fitness, trades, step);
     } else {
-        // a few episodes: one 16-wave workgroup each (4096-tick windows, the
-        // phases spread over the whole CU); many episodes: 4-wave workgroups
-        // (1024-tick windows), up to eight resident per CU, so the serial
-        // walks of different episodes overlap instead of idling the CU
-        const bool many = eps->n > kScanManyAbove;
-        const int nt = many ? kScanSmall : kScanThreads;
+        // the workgroup shrinks as episodes grow: few episodes get a 16-wave
+        // workgroup each (4096-tick windows, the phases spread over the CU);
+        // many get 8- or 4-wave ones (2048- / 1024-tick windows), several
+        // resident per CU, so the serial walks of different episodes overlap
+        // instead of idling the CU (A/B on MI355X: P=64 / 256 / 1024 / 4096)
+        const int nt = scan_threads(eps->n);
         size_t lds = (size_t)nt * kSumTpt * sizeof(double);
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
-        if (nsi <= 5 && many)
-            SGMM_LAUNCH((k_path_scan<5, kScanSmall>), dim3(eps->n), dim3(nt), lds, s, ep, params,
-                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
-        else if (nsi <= 5)
-            SGMM_LAUNCH((k_path_scan<5, kScanThreads>), dim3(eps->n), dim3(nt), lds, s, ep, params,
-                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
-        else if (many)
-            SGMM_LAUNCH((k_path_scan<8, kScanSmall>), dim3(eps->n), dim3(nt), lds, s, ep, params,
-                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+        if (nsi <= 5)
+            launch_path_scan<5>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, rew, fitness,
+                                trades, step);
         else
-            SGMM_LAUNCH((k_path_scan<8, kScanThreads>), dim3(eps->n), dim3(nt), lds, s, ep, params,
-                        eps->inv_min, cmaps, ctr, rew, fitness, trades, step);
+            launch_path_scan<8>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, rew, fitness,
+                                trades, step);
     }
     SGMM_LAUNCHED();
     return SGMM_OK;

@@ -205,13 +205,15 @@ def test_bench_config_population(sgmm, oracle):
     assert np.array_equal(fit, want_f)
 
 
-def test_many_episode_scan(sgmm, oracle):
-    """More than 512 episodes take the 4-wave path scan (1024-tick windows):
-    ragged lengths around its window boundaries, every episode bit-exact."""
+@pytest.mark.parametrize("n_ep", [600, 1100])
+def test_many_episode_scan(sgmm, oracle, n_ep):
+    """More than 256 / 1024 episodes take the 8- / 4-wave path scan (2048- /
+    1024-tick windows): ragged lengths around their window boundaries, every
+    episode bit-exact."""
     from sgmm_amd import synthetic
     T, H = 5000, 16
     base = [0, 1, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3600, 4096, 5000]
-    lens = np.array([base[i % len(base)] if i < 96 else 700 + (37 * i) % 4300 for i in range(600)], np.int64)
+    lens = np.array([base[i % len(base)] if i < 96 else 700 + (37 * i) % 4300 for i in range(n_ep)], np.int64)
     P = len(lens)
     b = synthetic.bundle_510300(T, seed=3)
     st = synthetic.train_stats(b)
