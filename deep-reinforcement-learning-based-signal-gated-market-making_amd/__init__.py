@@ -15,6 +15,6 @@ from .model import (AdversaryPolicy, NeuroEvolution, TradingPolicy, genome_size,
                     genome_to_state_dict, hidden_from_genome)
 from .rollout import (EnvConfig, EpisodeBatch, RolloutEngine, TickStore,  # noqa: F401
                       adversary_forward, normalize_signals, params_tensor, policy_forward)
-from .drl_engine import DRLEngine, evaluate_individual, evaluate_population  # noqa: F401
+from .drl_engine import DRLEngine, MultiDRLEngine, evaluate_individual, evaluate_population  # noqa: F401
 
 __version__ = "0.1.0"

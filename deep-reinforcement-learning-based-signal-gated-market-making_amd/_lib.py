@@ -61,6 +61,14 @@ class AskedPopulation(ctypes.Structure):
                 ("seed", ctypes.c_uint64), ("i0", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
+class Populations(ctypes.Structure):
+    """sgmm_populations: K GA populations advanced together (device pointers)."""
+    _fields_ = [("n_pop", ctypes.c_int32), ("P", ctypes.c_int32), ("hidden", ctypes.c_int32),
+                ("history_cap", ctypes.c_int32)] + \
+        [(n, ctypes.c_void_p) for n in ("states", "masters_mm", "masters_adv", "best_masters", "seeds",
+                                        "history")]
+
+
 class DayStreams(ctypes.Structure):
     _fields_ = [("n_days", ctypes.c_int32), ("pad_", ctypes.c_int32), ("tick_total", ctypes.c_int64)] + \
         [(n, ctypes.c_void_p) for n in ("snap_off", "snap_time", "bid", "ask", "bidvol", "askvol",
@@ -83,6 +91,7 @@ class GAHistory(ctypes.Structure):
 assert ctypes.sizeof(EnvParams) == 48
 assert ctypes.sizeof(GAState) == 80
 assert ctypes.sizeof(GAHistory) == 40
+assert ctypes.sizeof(Populations) == 64
 
 _VP, _I32, _I64, _U32, _U64, _D, _SZ = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                         ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
@@ -113,6 +122,13 @@ SIGNATURES = {
                                                   ctypes.c_size_t, _VP]),
     "sgmm_generation": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP, _VP, _VP, _VP, _VP,
                                        _I32, _U64, _I32, _VP, _VP, _VP, _I32, _VP, ctypes.c_size_t, _VP]),
+    "sgmm_generation_multi": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                             ctypes.POINTER(Populations), _VP, _VP, _VP, ctypes.c_size_t, _VP]),
+    "sgmm_rollout_fitness_asked_multi": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                                        ctypes.POINTER(Populations), _I32, _I32, _VP, _VP, _VP,
+                                                        ctypes.c_size_t, _VP]),
+    "sgmm_ga_step_multi": (ctypes.c_int, [ctypes.POINTER(Populations), _VP, _VP, _VP, _VP, _I64, _I64, _I32,
+                                          _I64, _VP]),
     "sgmm_event_bars_workspace_size": (ctypes.c_size_t, [_I64]),
     "sgmm_event_bars_build": (ctypes.c_int, [ctypes.POINTER(DayStreams), ctypes.POINTER(EventBars), _VP,
                                              ctypes.c_size_t, _VP]),

@@ -180,9 +180,67 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step(
                 n_adv, seed, history, hist_cap, next_mm, next_adv, i0, n, sv, si, lm, la);
 }
 
+// One workgroup per population (sgmm_ga_step_multi): population k's records
+// at byte offsets k * fit_ps / k * tr_ps, its state / masters / history / key
+// at index k.
+struct PopsArg {
+    sgmm_ga_state* states;
+    float* masters_mm;
+    float* masters_adv;
+    float* best_masters;
+    const uint64_t* seeds;
+    sgmm_ga_history* history;
+    int32_t hist_cap;
+    int32_t P;
+    int64_t n_mm, n_adv;
+};
+
+template <class T>
+__device__ __forceinline__ const T* at_bytes(const T* p, int64_t off) {
+    return p ? reinterpret_cast<const T*>(reinterpret_cast<const char*>(p) + off) : nullptr;
+}
+
+__global__ __launch_bounds__(kStepBlock) void k_ga_step_multi(
+    PopsArg pa, const double* __restrict__ fit, const int32_t* __restrict__ trades,
+    const double* __restrict__ vfit, const int32_t* __restrict__ vtrades, int64_t fit_ps,
+    int64_t tr_ps, ShardView shard) {
+    __shared__ double sv[2 * kStepBlock];
+    __shared__ int si[2 * kStepBlock];
+    __shared__ float lm[kMaxStepParams];
+    __shared__ float la[kMaxStepParams];
+    const int k = blockIdx.x;
+    ga_step_dev<false>(pa.states + k, at_bytes(fit, k * fit_ps), at_bytes(trades, k * tr_ps),
+                       at_bytes(vfit, k * fit_ps), at_bytes(vtrades, k * tr_ps), pa.P, shard,
+                       pa.masters_mm + k * pa.n_mm, pa.masters_adv ? pa.masters_adv + k * pa.n_adv : nullptr,
+                       pa.best_masters ? pa.best_masters + k * pa.n_mm : nullptr, pa.n_mm, pa.n_adv, pa.seeds[k],
+                       pa.history ? pa.history + (int64_t)k * pa.hist_cap : nullptr, pa.hist_cap, nullptr,
+                       nullptr, 0, 0, sv, si, lm, la);
+}
+
 }  // namespace sgmm
 
 using namespace sgmm;
+
+extern "C" int sgmm_ga_step_multi(const sgmm_populations* pops, const double* fitness,
+                                  const int32_t* trades, const double* val_fitness,
+                                  const int32_t* val_trades, int64_t fit_pop_stride,
+                                  int64_t trades_pop_stride, int32_t shard_n, int64_t shard_stride,
+                                  void* stream) {
+    clear_error();
+    SGMM_REQUIRE(pops && pops->n_pop > 0 && pops->P > 0, "bad populations");
+    SGMM_REQUIRE(supported_hidden(pops->hidden), "hidden=%d unsupported", pops->hidden);
+    SGMM_REQUIRE(pops->states && pops->masters_mm && pops->seeds && fitness && val_fitness, "null pointer");
+    SGMM_REQUIRE(shard_n <= 0 || shard_stride >= 8LL * shard_n, "shard_stride < 8 * shard_n");
+    const int64_t n_mm = (int64_t)pops->hidden * pops->hidden + 7 * pops->hidden + 2;
+    PopsArg pa{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, pops->seeds,
+               pops->history, pops->history_cap, pops->P, n_mm, pops->masters_adv ? 1250 : 0};
+    ProfScope prof("ga_step", as_stream(stream));
+    hipLaunchKernelGGL(k_ga_step_multi, dim3(pops->n_pop), dim3(kStepBlock), 0, as_stream(stream), pa,
+                       fitness, trades, val_fitness, val_trades, fit_pop_stride, trades_pop_stride,
+                       ShardView{shard_n, shard_stride});
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
 
 extern "C" int sgmm_ga_step(sgmm_ga_state* state, const double* fitness, const int32_t* trades,
                             const double* val_fitness, const int32_t* val_trades, int32_t P,

@@ -57,7 +57,9 @@ struct EpArrays {
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
 // the current generation's ask() of the GA state, generated in the kernel
 // (never written to memory): individual i0 + genome[e], values identical to
-// what sgmm_ga_ask writes.
+// what sgmm_ga_ask writes.  With several populations (pop_eps > 0) episode e
+// belongs to population k = e / pop_eps, whose state, masters and Philox key
+// sit at st + k, master_* + k * *_pstride and seeds[k].
 struct GenomeSrc {
     const float* mm;
     int64_t mm_stride;
@@ -66,32 +68,42 @@ struct GenomeSrc {
     const sgmm_ga_state* st;
     const float* master_mm;
     const float* master_adv;
-    uint64_t seed;
+    uint64_t seed;            // population 0's key when seeds == nullptr
     int32_t i0;
+    int32_t pop_eps;          // episodes per population (0: one population)
+    const uint64_t* seeds;    // [K] per-population keys, or nullptr
+    int64_t mm_pstride, adv_pstride;
 };
 
 constexpr int kAdvParams = 74;  // AdversaryPolicy weights = first 74 floats of the genome
+constexpr int kAdvGenome = 1250;  // adversary evolver masters are TradingPolicy() genomes (model.py:63)
 
-// Stage the policy genome (n floats) of individual gi and, when ga != nullptr
-// and ai >= 0, the adversary weights of individual ai into LDS.  Every thread
-// of the block calls; the caller synchronizes.
-__device__ void stage_genomes(const GenomeSrc& src, int gi, int ai, int n, float* gs, float* ga) {
+// Stage the policy genome (n floats) of individual gi of episode e's
+// population and, when ga != nullptr and ai >= 0, the adversary weights of
+// individual ai into LDS.  Every thread of the block calls; the caller
+// synchronizes.
+__device__ void stage_genomes(const GenomeSrc& src, int e, int gi, int ai, int n, float* gs, float* ga) {
     const int tid = threadIdx.x, nt = blockDim.x;
     if (src.st) {
-        const uint32_t gen = (uint32_t)src.st->gen;
-        const float sig = (float)src.st->sigma_mm;
+        const int k = src.pop_eps > 0 ? e / src.pop_eps : 0;
+        const sgmm_ga_state* st = src.st + k;
+        const uint64_t seed = src.seeds ? src.seeds[k] : src.seed;
+        const float* master = src.master_mm + (int64_t)k * src.mm_pstride;
+        const uint32_t gen = (uint32_t)st->gen;
+        const float sig = (float)st->sigma_mm;
         for (int k4 = tid; k4 < (n + 3) / 4; k4 += nt) {
             float v[4];
-            ask_row4(src.master_mm, n, sig, src.seed, 0u, gen, (uint32_t)(src.i0 + gi), k4, v);
+            ask_row4(master, n, sig, seed, 0u, gen, (uint32_t)(src.i0 + gi), k4, v);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (4 * k4 + q < n) gs[4 * k4 + q] = v[q];
         }
         if (ga && ai >= 0) {
-            const float siga = (float)src.st->sigma_adv;
+            const float siga = (float)st->sigma_adv;
+            const float* amaster = src.master_adv + (int64_t)k * src.adv_pstride;
             for (int k4 = tid; k4 < (kAdvParams + 3) / 4; k4 += nt) {
                 float v[4];
-                ask_row4(src.master_adv, kAdvParams, siga, src.seed, 1u, gen, (uint32_t)(src.i0 + ai), k4, v);
+                ask_row4(amaster, kAdvParams, siga, seed, 1u, gen, (uint32_t)(src.i0 + ai), k4, v);
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     if (4 * k4 + q < kAdvParams) ga[4 * k4 + q] = v[q];
@@ -179,7 +191,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     __shared__ float gsm[GenomeLayout<H>::N];
     __shared__ float gsa[kAdvParams];
     const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
-    stage_genomes(src, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
+    stage_genomes(src, e, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
     const float* g = gsm;
 
     __shared__ float sx[2][kChunk];
@@ -373,7 +385,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     __shared__ __attribute__((aligned(16))) float gsm[GenomeLayout<H>::N];
     __shared__ float gsa[kAdvParams];
     const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
-    stage_genomes(src, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
+    stage_genomes(src, e, ep.genome[e], ai, GenomeLayout<H>::N, gsm, ARL ? gsa : nullptr);
     __syncthreads();
     // layer-3 weights interleaved (W3[0][j], W3[1][j]) for the packed output chains
     __shared__ __attribute__((aligned(8))) float w3i[2 * H];
@@ -889,7 +901,13 @@ struct StepArgs {
     uint64_t seed;
     sgmm_ga_history* history;
     int32_t hist_cap;
-    int32_t P;          // fitness[0..P): training, fitness[P..2P): validation
+    int32_t P;          // per population: fitness[0..P) training, fitness[P..2P) validation
+    // several populations: episode e (workgroup e) belongs to population
+    // k = e / pop_eps, whose state / masters / history / key sit at st + k,
+    // master_* + k * n_*, history + k * hist_cap, seeds[k]; its records at
+    // fitness + k * pop_eps.  pop_eps == 0: one population (the whole grid).
+    int32_t pop_eps;
+    const uint64_t* seeds;
 };
 
 // LDS bytes the tail needs (aliased onto the kernel's dynamic LDS)
@@ -913,16 +931,28 @@ __device__ __forceinline__ void store_record(double* fitness, int32_t* trades, i
 // draws the last ticket reads every record with sc1 loads (ga_step_dev
 // <HANDOFF = true>) -- MI355X_MICROARCH.md inter-workgroup visibility, row 1
 // -- runs the GA step and resets the ticket for the next launch.
-__device__ void generation_tail(const StepArgs& sa, const double* fitness, const int32_t* trades,
+__device__ void generation_tail(const StepArgs& sa0, const double* fitness0, const int32_t* trades0,
                                 unsigned char* lds, int* s_last) {
+    // this workgroup's population (one arrival ticket per population)
+    const int n_eps = sa0.pop_eps > 0 ? sa0.pop_eps : (int)gridDim.x;
+    const int k = sa0.pop_eps > 0 ? (int)blockIdx.x / sa0.pop_eps : 0;
+    StepArgs sa = sa0;
+    sa.st = sa0.st + k;
+    sa.master_mm = sa0.master_mm + (int64_t)k * sa0.n_mm;
+    if (sa0.master_adv) sa.master_adv = sa0.master_adv + (int64_t)k * sa0.n_adv;
+    if (sa0.best_master) sa.best_master = sa0.best_master + (int64_t)k * sa0.n_mm;
+    if (sa0.history) sa.history = sa0.history + (int64_t)k * sa0.hist_cap;
+    const double* fitness = fitness0 + (int64_t)k * n_eps;
+    const int32_t* trades = trades0 + (int64_t)k * n_eps;
     if (threadIdx.x == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int prev = __hip_atomic_fetch_add(&sa.st->arrivals, 1, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = prev == (int)gridDim.x - 1;
+        *s_last = prev == n_eps - 1;
     }
     __syncthreads();
     if (!*s_last) return;
+    if (sa0.seeds) sa.seed = sa0.seeds[k];
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: loads after the ticket
     SGMM_STAMP(blockIdx.x, 4);
 #ifdef SGMM_STAMPS
@@ -1554,6 +1584,63 @@ extern "C" int sgmm_generation(const sgmm_ticks* ticks, const sgmm_episodes* eps
                   history_cap, P};
     return rollout_impl(ticks, eps, params, src, arl, hidden, fitness, trades, workspace,
                         workspace_bytes, step, as_stream(stream));
+}
+
+static int check_pops(const sgmm_populations* pops) {
+    SGMM_REQUIRE(pops, "null populations");
+    SGMM_REQUIRE(pops->n_pop > 0 && pops->P > 0, "n_pop=%d P=%d must be > 0", pops->n_pop, pops->P);
+    SGMM_REQUIRE(supported_hidden(pops->hidden), "hidden=%d unsupported (8,16,32,64)", pops->hidden);
+    SGMM_REQUIRE(pops->states && pops->masters_mm && pops->seeds, "null states / masters / seeds");
+    SGMM_REQUIRE(pops->history_cap >= 0 && (pops->history || pops->history_cap == 0), "history");
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_generation_multi(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                                     const sgmm_env_params* params, const sgmm_populations* pops,
+                                     double* fitness, int32_t* trades, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+    clear_error();
+    if (int rc = check_pops(pops)) return rc;
+    const int32_t H = pops->hidden, K = pops->n_pop, P = pops->P;
+    if (int rc = check_episodes(ticks, eps, params, pops->masters_mm, H)) return rc;
+    SGMM_REQUIRE((int64_t)eps->n == 2LL * K * P,
+                 "episodes must be n_pop x (P training + P validation) = %lld, got %d",
+                 2LL * K * P, eps->n);
+    const int64_t n_mm = (int64_t)H * H + 7 * H + 2;
+    SGMM_REQUIRE(n_mm <= kMaxStepParams, "genome too large for the fused GA step");
+    const bool arl = pops->masters_adv != nullptr;
+    const int64_t n_adv = arl ? kAdvGenome : 0;
+    GenomeSrc src{nullptr, 0, nullptr, 0, pops->states, pops->masters_mm, pops->masters_adv, 0, 0};
+    src.pop_eps = 2 * P;
+    src.seeds = pops->seeds;
+    src.mm_pstride = n_mm;
+    src.adv_pstride = n_adv;
+    StepArgs step{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, n_mm, n_adv, 0,
+                  pops->history, pops->history_cap, P, 2 * P, pops->seeds};
+    return rollout_impl(ticks, eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes, step,
+                        as_stream(stream));
+}
+
+extern "C" int sgmm_rollout_fitness_asked_multi(const sgmm_ticks* ticks, const sgmm_episodes* eps,
+                                                const sgmm_env_params* params,
+                                                const sgmm_populations* pops, int32_t i0,
+                                                int32_t n_eps_pop, double* fitness, int32_t* trades,
+                                                void* workspace, size_t workspace_bytes,
+                                                void* stream) {
+    clear_error();
+    if (int rc = check_pops(pops)) return rc;
+    const int32_t H = pops->hidden, K = pops->n_pop;
+    if (int rc = check_episodes(ticks, eps, params, pops->masters_mm, H)) return rc;
+    SGMM_REQUIRE(i0 >= 0 && n_eps_pop > 0 && (int64_t)eps->n == (int64_t)K * n_eps_pop,
+                 "episodes must be n_pop x n_eps_pop (i0=%d, n_eps_pop=%d, n=%d)", i0, n_eps_pop, eps->n);
+    const bool arl = pops->masters_adv != nullptr;
+    GenomeSrc src{nullptr, 0, nullptr, 0, pops->states, pops->masters_mm, pops->masters_adv, 0, i0};
+    src.pop_eps = n_eps_pop;
+    src.seeds = pops->seeds;
+    src.mm_pstride = (int64_t)H * H + 7 * H + 2;
+    src.adv_pstride = arl ? kAdvGenome : 0;
+    return rollout_impl(ticks, eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
+                        StepArgs{}, as_stream(stream));
 }
 
 extern "C" int sgmm_rollout_trace(const sgmm_ticks* ticks, const sgmm_episodes* eps,

@@ -502,6 +502,278 @@ class TrainingSession:
         return e.mm_evolver.master_policy, self.history
 
 
+class MultiDRLEngine:
+    """K independent DRLEngine.train runs advanced together on the GPU.
+
+    The reference trains one GA per inventory penalty phi (the lambda sweep:
+    run_agent_training_pipeline per PHI, main.py:39-45 ->
+    agent_trainer.py:136-137; checkpoints/688981/agent_best_val_{phi}.pth) and
+    one per asset (agent_trainer.py:168-173).  Here the K runs share every
+    generation's launches: population k keeps its own master, sigma schedule,
+    no-improvement counter, best validation reward, history, checkpoint path
+    ``{save_dir}/{prefix}_best_val_{phi}.pth`` and Philox key, so its results
+    are bit-identical to ``engines[k].train(...)`` run alone.
+
+    ``engines`` are configured DRLEngine objects (same pop_size, hidden_dim and
+    use_arl; rng="device"); ``MultiDRLEngine.sweep(phis, ...)`` builds one per
+    phi.  ``train`` takes one bundle (shared) or a list of K bundles (one per
+    population, e.g. per asset), likewise train_stats, and returns the list of
+    K (master_policy, history) results in engine order.
+    """
+
+    def __init__(self, engines):
+        self.engines = list(engines)
+        if not self.engines:
+            raise ValueError("MultiDRLEngine needs at least one DRLEngine")
+        e0 = self.engines[0]
+        for e in self.engines[1:]:
+            if (e.pop_size, e.hidden_dim, e.use_arl) != (e0.pop_size, e0.hidden_dim, e0.use_arl):
+                raise ValueError("populations of one MultiDRLEngine share pop_size, hidden_dim and use_arl")
+
+    @classmethod
+    def sweep(cls, phis, pop_size=50, sigma=0.05, tick_size=0.01, fee_rate=0.0, use_arl=False,
+              save_dir="checkpoints/drl", *, seeds=None, **kw):
+        """One DRLEngine per phi (the lambda sweep), constructed in phi order."""
+        engines = [DRLEngine(pop_size, sigma, phi, tick_size, fee_rate, use_arl, save_dir,
+                             seed=None if seeds is None else seeds[k], **kw)
+                   for k, phi in enumerate(phis)]
+        return cls(engines)
+
+    @property
+    def fused_path(self) -> bool:
+        """All populations on the one-launch device path (else: one after another)."""
+        return all(e.rng == "device" and e.val_mode in ("fused", "auto") and genome_size(e.hidden_dim) <= 4096
+                   for e in self.engines)
+
+    def session(self, train_bundles, val_bundles, train_stats, generations=100, output_prefix="agent"):
+        return MultiSession(self, train_bundles, val_bundles, train_stats, generations, output_prefix)
+
+    def train(self, train_bundles, val_bundles, train_stats, generations=100, output_prefix="agent"):
+        K = len(self.engines)
+        tr, va, st = (_per_pop(x, K) for x in (train_bundles, val_bundles, train_stats))
+        if not self.fused_path:  # reference order: one DRLEngine.train after another
+            return [e.train(tr[k], va[k], st[k], generations, output_prefix) for k, e in enumerate(self.engines)]
+        sess = self.session(tr, va, st, generations, output_prefix)
+        every = self.engines[0].sync_every
+        for gen in range(0, generations, every):
+            n = min(every, generations - gen)
+            sess.steps(gen, n)
+            if n == every:
+                sess.flush(gen + n)
+        return sess.finish()
+
+
+def _per_pop(x, K):
+    """One bundle / stats dict for all populations, or a list of K of them."""
+    if isinstance(x, dict) or (isinstance(x, tuple) and len(x) == 7 and not isinstance(x[0], (tuple, list))):
+        return [x] * K
+    x = list(x)
+    if len(x) != K:
+        raise ValueError(f"expected {K} per-population items, got {len(x)}")
+    return x
+
+
+class MultiSession:
+    """K DRLEngine.train runs resident on the GPU, one launch pair per
+    generation for all of them (sgmm_generation_multi), or -- with several
+    ranks -- the asked rollout of every population's shard, one all-gather of
+    the K records and one K-workgroup GA step (sgmm_ga_step_multi)."""
+
+    GRAPH_BATCH = TrainingSession.GRAPH_BATCH
+
+    def __init__(self, meng: MultiDRLEngine, train_bundles, val_bundles, train_stats, generations,
+                 output_prefix):
+        _lib.require_gpu()
+        engs = self.engs = meng.engines
+        e0 = engs[0]
+        K = self.K = len(engs)
+        tr, va, sts = (_per_pop(x, K) for x in (train_bundles, val_bundles, train_stats))
+        self.roll = RolloutEngine(e0.device or "cuda")
+        dev = self.dev = self.roll.device
+        self.L = self.roll.L
+        self.group, self.rank, self.world = _dist_info(e0.dist)
+        P, H = self.P, self.H = e0.pop_size, e0.hidden_dim
+        G = self.G = genome_size(H)
+        self.i0, self.i1 = shard_bounds(P, self.rank, self.world)
+        n_loc = self.n_loc = self.i1 - self.i0
+        n = self.n_cap = shard_capacity(P, self.world)
+        arl = self.arl = e0.use_arl
+        self.generations = int(generations)
+        # tick columns: each distinct (bundle, stats) once
+        self.ticks = TickStore()
+        seg_of = {}
+
+        def seg(b, s):
+            key = (id(b), id(s))
+            if key not in seg_of:
+                seg_of[key] = self.ticks.segments[self.ticks.add(b, s)]
+            return seg_of[key]
+
+        segs = [(seg(tr[k], sts[k]), seg(va[k], sts[k])) for k in range(K)]
+        self.ticks.to(dev)
+        self.T_tr = [s[0][1] for s in segs]
+        self.params = params_tensor([EnvConfig(phi=e.phi, tick_size=e.tick_size, fee_rate=e.fee_rate)
+                                     for e in engs], dev)
+        # episodes: per population n training slots then n validation slots
+        # (the shard's n_loc individuals first, zero-length pads after)
+        pad = n - n_loc
+        g, off, ln, par, adv = [], [], [], [], []
+        for k, ((to, T), (vo, Tv)) in enumerate(segs):
+            for o, L_, is_tr in ((to, T, True), (vo, Tv, False)):
+                g.append(np.concatenate([np.arange(n_loc), np.zeros(pad, np.int64)]))
+                off.append(np.full(n, o))
+                ln.append(np.concatenate([np.full(n_loc, L_), np.zeros(pad, np.int64)]))
+                par.append(np.full(n, k))
+                adv.append(g[-1] if is_tr else np.full(n, -1))  # validation: no adversary
+        self.eps = EpisodeBatch(np.concatenate(g), np.concatenate(off), np.concatenate(ln), np.concatenate(par),
+                                adv=np.concatenate(adv) if arl else None).to(dev)
+        self.rec = FitnessRecords(P, self.world, dev, n_pop=K)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.masters = torch.stack([e.mm_evolver.master_policy.get_weights() for e in engs]).to(**f32).contiguous()
+        self.masters_adv = torch.stack([e.adv_evolver.master_policy.get_weights() for e in engs]).to(**f32) \
+            .contiguous() if arl else None
+        self.best_masters = torch.zeros((K, G), **f32)
+        self.states = torch.zeros((K, HIST_STATE_SIZES[0]), dtype=torch.uint8, device=dev)
+        self.hist = torch.zeros((K, self.generations, HIST_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        self.seeds = torch.tensor([int(e.seed) for e in engs], dtype=torch.int64).to(dev)
+        for k, e in enumerate(engs):
+            if arl and e.adv_evolver.sigma != e.mm_evolver.sigma:
+                raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
+            check(self.L.sgmm_ga_state_init(ctypes.c_void_p(self.states[k].data_ptr()), float(e.mm_evolver.sigma),
+                                            e.patience, e.decay, stream_ptr()), "sgmm_ga_state_init")
+        self.pops = _lib.Populations(K, P, H, self.generations, self.states.data_ptr(), self.masters.data_ptr(),
+                                     self.masters_adv.data_ptr() if arl else None, self.best_masters.data_ptr(),
+                                     self.seeds.data_ptr(), self.hist.data_ptr())
+        self.use_graph = bool(e0.use_graph)
+        self.graphs = None
+        self.batch_graph = None
+        self.graph_batch = max(1, min(self.GRAPH_BATCH, e0.sync_every))
+        self.roll.reserve(self.eps, arl)
+        self.best_paths = [os.path.join(e.save_dir, f"{output_prefix}_best_val_{e.phi}.pth") for e in engs]
+        self.saved_any = [False] * K
+        self.emitted = 0
+        self.history = [{"gen": [], "train_f": [], "val_f": [], "train_trades": [], "val_trades": []}
+                        for _ in range(K)]
+
+    # one generation: rollout (+ GA step in its tail on one process)
+    def _rollout(self):
+        tk, ep = self.ticks.struct(), self.eps.struct()
+        ws = self.roll.workspace(self.eps, self.arl)
+        f, t = self.rec.both
+        if self.world == 1:
+            check(self.L.sgmm_generation_multi(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
+                                               ctypes.byref(self.pops), ptr(f), ptr(t), ptr(ws), ws.numel(),
+                                               stream_ptr()), "sgmm_generation_multi")
+        else:
+            check(self.L.sgmm_rollout_fitness_asked_multi(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
+                                                          ctypes.byref(self.pops), self.i0, 2 * self.n_cap,
+                                                          ptr(f), ptr(t), ptr(ws), ws.numel(), stream_ptr()),
+                  "sgmm_rollout_fitness_asked_multi")
+
+    def _exchange(self):
+        if self.world > 1:
+            self.rec.all_gather(self.group)
+
+    def _boundary(self):
+        if self.world > 1:
+            check(self.L.sgmm_ga_step_multi(ctypes.byref(self.pops), *self.rec.multi_step_args(), stream_ptr()),
+                  "sgmm_ga_step_multi")
+
+    def capture(self):
+        if not self.use_graph:
+            return
+        if self.graphs is None:
+            self.graphs = []
+            phases = [(self._rollout,)] if self.world == 1 else [(self._rollout,), (self._boundary,)]
+            for fns in phases:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for fn in fns:
+                        fn()
+                self.graphs.append(g)
+        if self.world == 1 and self.graph_batch > 1 and self.batch_graph is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.graph_batch):
+                    self._rollout()
+            self.batch_graph = g
+
+    def step(self, gen: int):
+        if not self.use_graph:
+            self._rollout()
+            self._exchange()
+            self._boundary()
+            return
+        self.capture()
+        self.graphs[0].replay()
+        if self.world > 1:
+            self._exchange()
+            self.graphs[1].replay()
+
+    def steps(self, gen0: int, n: int):
+        if not self.use_graph or self.world > 1:
+            for g in range(gen0, gen0 + n):
+                self.step(g)
+            return
+        B, done = self.graph_batch, 0
+        if B > 1 and n >= B:
+            self.capture()
+            while n - done >= B:
+                self.batch_graph.replay()
+                done += B
+        for g in range(gen0 + done, gen0 + n):
+            self.step(g)
+
+    def flush(self, upto: int):
+        """History rows [emitted, upto) of every population: the reference's log
+        lines (prefixed with the population's phi), checkpoints."""
+        if upto <= self.emitted:
+            return
+        rows_all = self.hist[:, self.emitted:upto].cpu().numpy()
+        for k, e in enumerate(self.engs):
+            rows = rows_all[k].reshape(-1).view(HIST_DTYPE)
+            improved_any = False
+            h = self.history[k]
+            for j, r in enumerate(rows):
+                g = self.emitted + j
+                imp = bool(r["flags"] & 1)
+                improved_any |= imp
+                if r["flags"] & 2:
+                    e._log(f"[phi={e.phi}] >>> Sigma decayed to {r['sigma_after']:.4f} due to no improvement")
+                h["gen"].append(g)
+                h["train_f"].append(np.float64(r["train_f"]))
+                h["val_f"].append(np.float64(r["val_f"]))
+                h["train_trades"].append(int(r["train_trades"]))
+                h["val_trades"].append(int(r["val_trades"]))
+                if g % 5 == 0:
+                    tag = "ARL:ON" if self.arl else "ARL:OFF"
+                    e._log(f"[phi={e.phi}] Gen {g:03d} | {tag} | Best Train: {r['train_f']:.2f} | "
+                           f"Val: {r['val_f']:.2f}{'*' if imp else ''}")
+            if improved_any and self.rank == 0:
+                torch.save(genome_to_state_dict(self.best_masters[k], self.H), self.best_paths[k])
+            self.saved_any[k] |= improved_any
+        self.emitted = upto
+
+    def finish(self):
+        self.flush(self.generations)
+        torch.cuda.synchronize()
+        st = self.states.cpu().numpy().reshape(-1).view(STATE_DTYPE)
+        out = []
+        for k, e in enumerate(self.engs):
+            e.mm_evolver.sigma = float(st[k]["sigma_mm"])
+            e.mm_evolver.master_policy.set_weights(self.masters[k].cpu())
+            if self.arl:
+                e.adv_evolver.sigma = float(st[k]["sigma_adv"])
+                e.adv_evolver.master_policy.set_weights(self.masters_adv[k].cpu())
+            if self.saved_any[k]:
+                e.mm_evolver.master_policy.load_state_dict(genome_to_state_dict(self.best_masters[k], self.H))
+            elif os.path.exists(self.best_paths[k]):
+                e.mm_evolver.master_policy.load_state_dict(torch.load(self.best_paths[k], weights_only=True))
+            e.timing = {"generations": self.generations}
+            out.append((e.mm_evolver.master_policy, self.history[k]))
+        return out
+
+
 # ---------------------------------------------------------------------- small helpers
 def ctypes_size(t):
     import ctypes

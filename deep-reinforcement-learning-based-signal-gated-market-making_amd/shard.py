@@ -51,20 +51,26 @@ def element_offset(i: int, n: int, field: str) -> int:
 
 
 class FitnessRecords:
-    """The rank's record and the gathered records of all ranks."""
+    """The rank's record and the gathered records of all ranks.
 
-    def __init__(self, P: int, world: int, device):
-        self.P, self.world = int(P), int(world)
+    With K populations (n_pop) the record holds every population's shard:
+    f64 fitness[K][2n] then i32 trades[K][2n] (24 K n bytes); population k's
+    fields sit at k * 16n (fitness) and 16Kn + k * 8n (trades) -- K = 1 is the
+    single-population layout above."""
+
+    def __init__(self, P: int, world: int, device, n_pop: int = 1):
+        self.P, self.world, self.K = int(P), int(world), int(n_pop)
         n = self.n = shard_capacity(P, world)
+        K = self.K
         self.device = torch.device(device)
-        self.rec = torch.zeros(record_bytes(n), dtype=torch.uint8, device=self.device)
-        f = self.rec[:16 * n].view(torch.float64)
-        t = self.rec[16 * n:].view(torch.int32)
+        self.rec = torch.zeros(K * record_bytes(n), dtype=torch.uint8, device=self.device)
+        f = self.rec[:16 * K * n].view(torch.float64)
+        t = self.rec[16 * K * n:].view(torch.int32)
         self.f, self.t = f, t
         self.train = (f[:n], t[:n])
-        self.val = (f[n:], t[n:])
-        self.both = (f, t)  # train then validation, for one fused launch of 2n episodes
-        self.gathered = torch.zeros(world * record_bytes(n), dtype=torch.uint8, device=self.device) \
+        self.val = (f[n:2 * n], t[n:2 * n])
+        self.both = (f, t)  # per population train then validation, for one fused launch
+        self.gathered = torch.zeros(world * K * record_bytes(n), dtype=torch.uint8, device=self.device) \
             if world > 1 else None
         self._host = None
 
@@ -96,6 +102,19 @@ class FitnessRecords:
         ptrs = tuple(ctypes.c_void_p(base + lay[k][0]) for k in ("train_f", "train_t", "val_f", "val_t"))
         shard = (0, 0) if self.world == 1 else (n, record_bytes(n))
         return ptrs + (self.P,) + shard
+
+    def multi_step_args(self):
+        """(fit, trades, val_fit, val_trades, fit_pop_stride, trades_pop_stride,
+        shard_n, shard_stride): the arguments of sgmm_ga_step_multi --
+        population 0's field pointers into the gathered records (or the local
+        record when world == 1) and the per-population byte strides."""
+        import ctypes
+        n, K = self.n, self.K
+        base = (self.rec if self.world == 1 else self.gathered).data_ptr()
+        offs = (0, 16 * K * n, 8 * n, 16 * K * n + 4 * n)  # train_f, train_t, val_f, val_t
+        ptrs = tuple(ctypes.c_void_p(base + o) for o in offs)
+        shard = (0, 0) if self.world == 1 else (n, K * record_bytes(n))
+        return ptrs + (16 * n, 8 * n) + shard
 
     def population(self):
         """Contiguous (train_f f64[P], train_t i32[P], val_f, val_t) of the whole

@@ -276,6 +276,61 @@ int sgmm_generation(const sgmm_ticks *ticks, const sgmm_episodes *eps,
                     int32_t P, double *fitness, int32_t *trades, sgmm_ga_history *history,
                     int32_t history_cap, void *workspace, size_t workspace_bytes, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Several GA populations advanced together: one DRLEngine.train per
+ * inventory penalty phi (the lambda sweep of pipeline/agent_trainer.py:136-137
+ * called per phi at main.py:39-45; checkpoints/688981/agent_best_val_{phi}.pth)
+ * or per asset (agent_trainer.py:168-173).  Population k keeps its own
+ * master, sigma schedule, no-improvement counter, best validation reward,
+ * history and Philox key -- exactly the state of an independent DRLEngine
+ * run with seed seeds[k], so K populations in one launch reproduce K
+ * separate runs bit for bit.  A HOST struct whose members point to device
+ * memory; rows are contiguous per population.
+ * ------------------------------------------------------------------------ */
+typedef struct sgmm_populations {
+    int32_t n_pop;              /* K */
+    int32_t P;                  /* individuals per population (global, all ranks) */
+    int32_t hidden;             /* TradingPolicy hidden width (every population) */
+    int32_t history_cap;        /* history rows per population */
+    sgmm_ga_state *states;      /* [K] (sgmm_ga_state_init each) */
+    float *masters_mm;          /* [K][H*H+7H+2] */
+    float *masters_adv;         /* [K][1250] or NULL (no adversary) */
+    float *best_masters;        /* [K][H*H+7H+2] checkpoint slots (drl_engine.py:144-150) */
+    const uint64_t *seeds;      /* [K] device: per-population Philox key */
+    sgmm_ga_history *history;   /* [K][history_cap] */
+} sgmm_populations;             /* 64 bytes */
+
+/* One generation of K populations on one process.  Episodes: population k
+ * owns episodes [2Pk, 2Pk+P) (training, individual genome[e]) and
+ * [2Pk+P, 2P(k+1)) (validation, individual genome[e]); each episode's
+ * params[param[e]] carries that population's phi / tick / fee.  The last
+ * workgroup of each population runs its generation boundary (sgmm_ga_step).
+ * fitness/trades: [K*2P], population-major.  Two kernel launches.
+ * n_pop = 1 is sgmm_generation with seed = seeds[0]. */
+int sgmm_generation_multi(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                          const sgmm_env_params *params, const sgmm_populations *pops,
+                          double *fitness, int32_t *trades, void *workspace,
+                          size_t workspace_bytes, void *stream);
+
+/* A rank's shard of K asked populations (multi-GPU): population k owns
+ * episodes [k*n_eps_pop, (k+1)*n_eps_pop) of the batch, individual
+ * i0 + genome[e] of population k; fitness/trades [eps->n]. */
+int sgmm_rollout_fitness_asked_multi(const sgmm_ticks *ticks, const sgmm_episodes *eps,
+                                     const sgmm_env_params *params, const sgmm_populations *pops,
+                                     int32_t i0, int32_t n_eps_pop, double *fitness,
+                                     int32_t *trades, void *workspace, size_t workspace_bytes,
+                                     void *stream);
+
+/* sgmm_ga_step for each of the K populations (one workgroup each, one
+ * launch): population k reads its records at byte offset k * fit_pop_stride
+ * from fitness / val_fitness and k * trades_pop_stride from trades /
+ * val_trades, with the shard addressing of sgmm_ga_step (shard_n,
+ * shard_stride) inside. */
+int sgmm_ga_step_multi(const sgmm_populations *pops, const double *fitness, const int32_t *trades,
+                       const double *val_fitness, const int32_t *val_trades,
+                       int64_t fit_pop_stride, int64_t trades_pop_stride, int32_t shard_n,
+                       int64_t shard_stride, void *stream);
+
 /* Sequential float64 sum init + values[0] + values[1] + ... (device array,
  * result written to *out on the stream): the episode total of
  * Env/drl_engine.py:53 (total_reward += reward), evaluated in parallel and

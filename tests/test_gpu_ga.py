@@ -150,14 +150,17 @@ def _bundles(seed=0, T=600, Tv=150):
     return tr, va, synthetic.train_stats(tr)
 
 
-@pytest.mark.parametrize("arl", [False, True])
-def test_device_rng_modes_agree(sgmm, tmp_path, arl):
-    """graph replay == eager, fused validation == validate-the-best."""
+@pytest.mark.parametrize("arl,P", [(False, 24), (True, 24), (False, 200), (False, 600), (True, 600)])
+def test_device_rng_modes_agree(sgmm, tmp_path, arl, P):
+    """graph replay == eager, fused validation == validate-the-best.  P=24:
+    the 1024-thread scan's one-workgroup fused tail; P=200: 400 episodes, the
+    512-thread scan (fused tail with P <= 512 threads); P=600: 1200 episodes,
+    the 256-thread scan whose tail runs the general GA step."""
     tr, va, st = _bundles()
     res = []
     for use_graph, val_mode in ((True, "fused"), (False, "fused"), (False, "best"), (True, "best")):
         torch.manual_seed(0)  # the initial master is drawn from the torch generator
-        eng = sgmm.DRLEngine(pop_size=24, phi=0.0005, tick_size=0.001, use_arl=arl,
+        eng = sgmm.DRLEngine(pop_size=P, phi=0.0005, tick_size=0.001, use_arl=arl,
                              save_dir=str(tmp_path / f"{use_graph}{val_mode}"), hidden_dim=16, rng="device",
                              seed=42, val_mode=val_mode, use_graph=use_graph, verbose=False, sync_every=7,
                              patience=4)

@@ -1,0 +1,87 @@
+"""GPU tests of MultiDRLEngine: K GA populations (the lambda sweep of
+BASELINE config 3, the per-asset runs of config 5) advanced in one launch pair
+per generation must equal K independent DRLEngine.train runs bit for bit --
+histories, final masters, sigma schedules and checkpoints
+(agent_trainer.py:136-137 per phi, main.py:39-45; agent_trainer.py:168-173)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import has_gpu
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+
+def _bundles():
+    from sgmm_amd import synthetic
+    a_tr = synthetic.bundle_510300(600, seed=10)
+    a_va = synthetic.bundle_510300(150, seed=11)
+    b_tr = synthetic.bundle_688981(520, seed=12)   # a second asset: other tick, other length
+    b_va = synthetic.bundle_688981(170, seed=13)
+    return (a_tr, a_va, synthetic.train_stats(a_tr)), (b_tr, b_va, synthetic.train_stats(b_tr))
+
+
+# population k: (phi, tick, asset)
+POPS = [(0.0001, 0.001, 0), (0.005, 0.001, 0), (0.01, 0.01, 1)]
+
+
+def _engine(sgmm, k, P, arl, save_dir, H=16):
+    phi, tick, _ = POPS[k]
+    torch.manual_seed(100 + k)  # the initial master (and adversary master) come from the torch generator
+    return sgmm.DRLEngine(pop_size=P, phi=phi, tick_size=tick, use_arl=arl, save_dir=save_dir, hidden_dim=H,
+                          rng="device", seed=1000 + 7 * k, val_mode="fused", sync_every=5, patience=3,
+                          verbose=False)
+
+
+@pytest.mark.parametrize("P,arl", [(24, False), (24, True), (300, False), (600, False)])
+def test_multi_equals_independent_runs(sgmm, tmp_path, P, arl):
+    """P=24: the tail's one-workgroup fused GA step; P=300/600 with 3 x 2P
+    episodes: the 256-thread path scan, whose tail runs the general step."""
+    assets = _bundles()
+    gens = 12
+    tr = [assets[a][0] for _, _, a in POPS]
+    va = [assets[a][1] for _, _, a in POPS]
+    st = [assets[a][2] for _, _, a in POPS]
+    multi = sgmm.MultiDRLEngine([_engine(sgmm, k, P, arl, str(tmp_path / "multi")) for k in range(len(POPS))])
+    assert multi.fused_path
+    res = multi.train(tr, va, st, generations=gens)
+    for k in range(len(POPS)):
+        single = _engine(sgmm, k, P, arl, str(tmp_path / f"single{k}"))
+        pol, hist = single.train(tr[k], va[k], st[k], generations=gens)
+        mpol, mhist = res[k]
+        for key in hist:
+            assert np.array_equal(np.array(mhist[key], np.float64), np.array(hist[key], np.float64),
+                                  equal_nan=True), (k, key)
+        assert np.array_equal(mpol.get_weights().numpy(), pol.get_weights().numpy()), k
+        me, se = multi.engines[k], single
+        assert me.mm_evolver.sigma == se.mm_evolver.sigma, k
+        if arl:
+            assert torch.equal(me.adv_evolver.master_policy.get_weights(),
+                               se.adv_evolver.master_policy.get_weights()), k
+        name = f"agent_best_val_{POPS[k][0]}.pth"
+        a = torch.load(os.path.join(tmp_path / "multi", name), weights_only=True)
+        b = torch.load(os.path.join(tmp_path / f"single{k}", name), weights_only=True)
+        assert all(torch.equal(a[x], b[x]) for x in b), k
+    # the populations are live and distinct
+    assert len({float(r[1]["train_f"][-1]) for r in res}) == len(POPS)
+
+
+def test_multi_sweep_constructor_and_shared_bundle(sgmm, tmp_path):
+    """MultiDRLEngine.sweep(phis) with one shared bundle == per-phi DRLEngines."""
+    (tr, va, st), _ = _bundles()
+    phis = [0.0001, 0.001, 0.005, 0.008, 0.01]
+    torch.manual_seed(5)
+    m = sgmm.MultiDRLEngine.sweep(phis, pop_size=16, tick_size=0.001, save_dir=str(tmp_path / "m"),
+                                  hidden_dim=16, seeds=[11, 12, 13, 14, 15], sync_every=4, verbose=False)
+    masters = [e.mm_evolver.master_policy.get_weights().clone() for e in m.engines]
+    res = m.train(tr, va, st, generations=8)
+    for k, phi in enumerate(phis):
+        e = sgmm.DRLEngine(pop_size=16, phi=phi, tick_size=0.001, save_dir=str(tmp_path / f"s{k}"), hidden_dim=16,
+                           seed=11 + k, sync_every=4, verbose=False)
+        e.mm_evolver.master_policy.set_weights(masters[k])
+        pol, hist = e.train(tr, va, st, generations=8)
+        assert np.array_equal(np.array(res[k][1]["train_f"]), np.array(hist["train_f"])), phi
+        assert np.array_equal(res[k][0].get_weights().numpy(), pol.get_weights().numpy()), phi

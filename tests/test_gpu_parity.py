@@ -205,11 +205,14 @@ def test_bench_config_population(sgmm, oracle):
     assert np.array_equal(fit, want_f)
 
 
+@pytest.mark.parametrize("caps", [(2, -2), (3, -4)], ids=["5states", "8states"])
 @pytest.mark.parametrize("n_ep", [600, 1100])
-def test_many_episode_scan(sgmm, oracle, n_ep):
+def test_many_episode_scan(sgmm, oracle, n_ep, caps):
     """More than 256 / 1024 episodes take the 8- / 4-wave path scan (2048- /
     1024-tick windows): ragged lengths around their window boundaries, every
-    episode bit-exact."""
+    episode bit-exact; with 5 inventory states (the default caps) and with 8
+    (i_max=3, i_min=-4: the NSM=8 scan instantiations)."""
+    i_max, i_min = caps
     from sgmm_amd import synthetic
     T, H = 5000, 16
     base = [0, 1, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3600, 4096, 5000]
@@ -222,12 +225,14 @@ def test_many_episode_scan(sgmm, oracle, n_ep):
     ticks = sgmm.TickStore()
     seg = ticks.add(b, st)
     ticks.to(DEV)
-    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0001, tick_size=0.001)], DEV)
-    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P)).to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0001, tick_size=0.001, i_max=i_max, i_min=i_min)], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
+                           inv_min=i_min, inv_max=i_max).to(DEV)
     fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
     want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,
                                            np.zeros(P), lens, np.zeros(P),
-                                           [oracle.params(phi=0.0001, tick=0.001)], n_threads=8)
+                                           [oracle.params(phi=0.0001, tick=0.001, i_max=i_max, i_min=i_min)],
+                                           n_threads=8)
     assert np.array_equal(trd.cpu().numpy(), want_t)
     assert np.array_equal(fit.cpu().numpy(), want_f)
 
