@@ -1,24 +1,38 @@
 #!/usr/bin/env python
 """Benchmark: env-steps/sec of the GA population rollout (BASELINE.json metric).
 
-One step = one GA generation of BASELINE config 2 on every GPU:
-  ask (population from master + sigma * N(0,1), on device)
-  -> rollout of the population's training episodes (+ fused validation
-     episodes of the same genomes) through sgmm_rollout_fitness
-  -> [N > 1: RCCL all-gather of fitness]
-  -> tell (argmax, new master) -> validation bookkeeping / sigma decay.
-Workload per GPU: population 64, TradingPolicy 3->16->16->2 (H=16), synthetic
-510300.SH-shaped ticks, 3600 training ticks + 720 validation ticks, phi=1e-4,
-tick 0.001, no adversary.  Weak scaling: each rank owns 64 individuals of a
-64*N population.  value = N * 64 * 3600 training env-steps per generation /
-measured seconds per generation (validation ticks are not counted).
+One step = one GA generation of every population on every GPU:
+  ask (population from master + sigma * N(0,1), generated inside the rollout)
+  -> rollout of the populations' training episodes (+ fused validation
+     episodes of the same genomes)
+  -> [N > 1: one RCCL all-gather of the fitness records]
+  -> tell (argmax, new master) -> validation bookkeeping / sigma decay,
+run through MultiDRLEngine (K populations in one launch pair per generation).
+value = training env-steps (population x training ticks, all populations,
+all ranks) per generation / measured seconds per generation; validation ticks
+are executed but not counted.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+Workloads (--config, BASELINE.json configs; synthetic SURVEY 8d ticks):
+  3 (default)  GA population 512 per lambda, lambda in {1e-4, 1e-3, 5e-3, 8e-3,
+               1e-2} (five populations), TradingPolicy 3->32->32->2 (the
+               reference's H), one full 510300.SH trading day at event_step=1
+               (4560 training ticks) + 912 validation ticks.  N > 1: weak
+               scaling, every rank owns 512 individuals of each population.
+  2            population 64, 3->16->16->2, 3600 + 720 ticks, phi 1e-4; weak.
+  4            adversarial co-training: 256 MM + 256 adversaries paired i<->i,
+               H=32, 3600 + 720 ticks; the 256 pairs split over the N ranks
+               (strong).
+  5            two assets (510300: tick 0.001, phi 1e-4; 688981: tick 0.01,
+               phi 1e-2) x population 4096, H=32, 3600 + 720 ticks; each
+               population split over the N ranks (strong).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 Rank 0 prints one JSON line.  The CPU baseline (rank 0, N=1 only) runs BEFORE
 the GPU is touched: the reference-equivalent batch-1 torch loop
-(oracle/ref_loop.py) under a fork Pool, on one generation of the same workload.
+(oracle/ref_loop.py) under fork Pools of 16 and 8 workers on a bounded sample
+of the same workload, plus the C oracle as a "best CPU" line.
 """
 from __future__ import annotations
 
@@ -36,25 +50,49 @@ sys.path.insert(0, str(ROOT))
 METRIC = "env-steps/sec (pop×ticks) at 1/2/4/8 MI355X; generations/sec vs CPU ref"
 FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA dense peak
 HBM_PEAK_GBPS = 8000.0     # MI355X_MICROARCH.md: HBM3E spec
+LAMBDAS = [0.0001, 0.001, 0.005, 0.008, 0.01]
+
+# config -> populations [(phi, tick, asset)], P (per population), H, T train, T val, ARL, scaling
+CONFIGS = {
+    2: dict(pops=[(0.0001, 0.001, "510300")], P=64, H=16, T=3600, Tv=720, arl=False, scaling="weak"),
+    3: dict(pops=[(l, 0.001, "510300") for l in LAMBDAS], P=512, H=32, T=4560, Tv=912, arl=False,
+            scaling="weak"),
+    4: dict(pops=[(0.0001, 0.001, "510300")], P=256, H=32, T=3600, Tv=720, arl=True, scaling="strong"),
+    5: dict(pops=[(0.0001, 0.001, "510300"), (0.01, 0.01, "688981")], P=4096, H=32, T=3600, Tv=720,
+            arl=False, scaling="strong"),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--pop", type=int, default=64, help="population per GPU")
-    ap.add_argument("--hidden", type=int, default=16)
-    ap.add_argument("--ticks", type=int, default=3600)
-    ap.add_argument("--val-ticks", type=int, default=720)
-    ap.add_argument("--phi", type=float, default=0.0001)
-    ap.add_argument("--profile-steps", type=int, default=20,
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(CONFIGS))
+    ap.add_argument("--pop", type=int, default=0, help="override: individuals per population (per GPU if weak)")
+    ap.add_argument("--hidden", type=int, default=0, help="override: TradingPolicy hidden width")
+    ap.add_argument("--ticks", type=int, default=0, help="override: training ticks")
+    ap.add_argument("--val-ticks", type=int, default=-1, help="override: validation ticks")
+    ap.add_argument("--profile-steps", type=int, default=5,
                     help="eager generations timed kernel by kernel with HIP events")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=0, help="0: min(16, cpu_count)")
-    ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest in profiles/)")
+    ap.add_argument("--cpu-episodes", type=int, default=64, help="episodes in the CPU-baseline sample")
+    ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest for this config)")
     return ap.parse_args()
+
+
+def workload_spec(args):
+    c = dict(CONFIGS[args.config])
+    if args.pop:
+        c["P"] = args.pop
+    if args.hidden:
+        c["H"] = args.hidden
+    if args.ticks:
+        c["T"] = args.ticks
+    if args.val_ticks >= 0:
+        c["Tv"] = args.val_ticks
+    return c
 
 
 def flop_per_step(H: int) -> int:
@@ -62,17 +100,39 @@ def flop_per_step(H: int) -> int:
     return 2 * (3 * H + H * H + 2 * H)
 
 
-def workload(args, seed=0):
+def bundles(spec, seed=0):
+    """{asset: (train bundle, validation bundle, train_stats)}, synthetic."""
     import sgmm_pkg
     sgmm_pkg.load()
     from sgmm_amd import synthetic
-    train = synthetic.bundle_510300(args.ticks, seed=seed)
-    val = synthetic.bundle_510300(args.val_ticks, seed=seed + 1, start_ticks=3500)
-    return train, val, synthetic.train_stats(train)
+    out = {}
+    for j, asset in enumerate(sorted({a for _, _, a in spec["pops"]})):
+        mk = synthetic.bundle_510300 if asset == "510300" else synthetic.bundle_688981
+        tr = mk(spec["T"], seed=seed + 10 * j)
+        va = mk(spec["Tv"], seed=seed + 10 * j + 1)
+        out[asset] = (tr, va, synthetic.train_stats(tr))
+    return out
 
 
-def cpu_baseline(args):
-    """Reference-equivalent CPU loop on one generation of the workload (before any GPU use)."""
+def describe(spec, world, P_glob):
+    pops = spec["pops"]
+    H = spec["H"]
+    cfg_match = {k: v for k, v in CONFIGS.items()
+                 if (v["P"], v["H"], v["T"], v["Tv"], v["pops"], v["arl"]) ==
+                 (spec["P"], H, spec["T"], spec["Tv"], pops, spec["arl"])}
+    head = f"BASELINE config {next(iter(cfg_match))}: " if cfg_match else "custom (not a BASELINE config): "
+    lam = ", ".join(f"phi={p} tick={t} {a}" for p, t, a in pops)
+    return (head + f"{len(pops)} GA population(s) x {P_glob} individuals ({lam}), "
+            f"TradingPolicy 3->{H}->{H}->2{' + AdversaryPolicy pairs' if spec['arl'] else ''}, synthetic ticks "
+            f"({spec['T']} train + {spec['Tv']} fused validation), {world} GPU(s), "
+            f"{spec['scaling']} scaling")
+
+
+def cpu_baseline(spec, n_episodes):
+    """Reference-equivalent CPU loop on a bounded sample of the workload,
+    before any GPU use: Pool(16) (the box's CPU share for one GPU) and
+    Pool(8) (the reference's hard-coded Pool(processes=8), drl_engine.py:91),
+    pools started and warmed up outside the timed map; plus the C oracle."""
     import numpy as np
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
@@ -80,39 +140,53 @@ def cpu_baseline(args):
     import sgmm_pkg
     sgmm_pkg.load()
     from sgmm_amd import synthetic
-    train, _, stats = workload(args)
-    pop = synthetic.population(args.pop, args.hidden, sigma=0.05, seed=7).numpy()
-    workers = args.cpu_workers or min(16, os.cpu_count() or 1)
-    fit, trd, dt, workers = ref_loop.population(pop, None, train, args.phi, 0.001, 0.0, stats,
-                                                args.hidden, workers=workers)
-    steps = args.pop * args.ticks
-    # the C restatement as a "best CPU" line (same sample, OpenMP threads)
-    s1n, s2n = oracle.normalize_signals(train[0], train[1], stats)
-    ticks = (s1n, s2n) + tuple(train[2:])
-    t0 = time.perf_counter()
-    cf, ct = oracle.evaluate_batch(pop, args.hidden, None, ticks, np.arange(args.pop), None,
-                                   np.zeros(args.pop), np.full(args.pop, args.ticks), np.zeros(args.pop),
-                                   [oracle.params(phi=args.phi, tick=0.001)], n_threads=workers)
-    dtc = time.perf_counter() - t0
-    same = bool(np.array_equal(np.array(trd), ct))
+    H = spec["H"]
+    phi0, tick, asset = spec["pops"][0]
+    tr, _, stats = bundles(spec)[asset]
+    n = max(16, n_episodes)
+    pop = synthetic.population(n, H, sigma=0.05, seed=7).numpy()
+    adv = synthetic.population(n, 32, sigma=0.05, seed=8).numpy() if spec["arl"] else None
+    phis = np.array([spec["pops"][i % len(spec["pops"])][0] if spec["pops"][i % len(spec["pops"])][2] == asset
+                     else phi0 for i in range(n)])
+    steps = n * spec["T"]
     try:
         cpu_model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         cpu_model = "unknown"
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": workers, "kind": "port",
-            "sample": (f"one generation of the bench workload ({args.pop} episodes x {args.ticks} ticks, "
-                       f"H={args.hidden}) through oracle/ref_loop.py (reference batch-1 torch loop "
-                       f"restated) on a fork Pool of {workers} workers, torch threads=1"),
-            "seconds": dt, "cpu_model": cpu_model,
-            "c_oracle": {"value": steps / dtc, "cores": workers, "seconds": dtc,
-                         "trades_agree_with_port": same}}
+    pools = {}
+    trades = None
+    for w in (16, 8):
+        w_eff = min(w, os.cpu_count() or 1)
+        with ref_loop.RefPool(pop, adv, tr, phis, tick, 0.0, stats, H, workers=w_eff) as rp:
+            f, t, dt = rp.map()
+        trades = t
+        pools[f"pool{w}"] = {"value": steps / dt, "cores": w_eff, "seconds": dt}
+    # the C restatement as a "best CPU" line (same sample, OpenMP threads)
+    s1n, s2n = oracle.normalize_signals(tr[0], tr[1], stats)
+    ticks = (s1n, s2n) + tuple(tr[2:])
+    plist = [oracle.params(phi=float(p), tick=tick) for p in phis]
+    t0 = time.perf_counter()
+    cf, ct = oracle.evaluate_batch(pop, H, adv, ticks, np.arange(n), np.arange(n) if adv is not None else None,
+                                   np.zeros(n), np.full(n, spec["T"]), np.arange(n), plist, n_threads=16)
+    dtc = time.perf_counter() - t0
+    best = pools["pool16"]
+    return {"value": best["value"], "unit": "env-steps/s", "cores": best["cores"], "kind": "port",
+            "sample": (f"{n} training episodes of the workload ({spec['T']} ticks, H={H}, "
+                       f"{'ARL pairs, ' if adv is not None else ''}phi cycling over the populations) through "
+                       f"oracle/ref_loop.py (the reference's batch-1 torch loop restated, validated against "
+                       f"reference fixtures) on a fork Pool, torch threads=1, pool start-up untimed"),
+            "pools": pools, "os_cpu_count": os.cpu_count(), "cpu_model": cpu_model,
+            "note": "Pool(16) = the CPU share of one GPU on this box (its process guard caps pools at 16); "
+                    "Pool(8) = the reference's Pool(processes=8)",
+            "c_oracle": {"value": steps / dtc, "cores": 16, "seconds": dtc,
+                         "trades_agree_with_port": bool(np.array_equal(np.array(trades), ct))}}
 
 
-def latest_pmc(path_arg):
+def latest_pmc(path_arg, config):
     if path_arg:
         p = Path(path_arg)
     else:
-        cands = sorted((ROOT / "profiles").glob("*pmc_traffic*.json"))
+        cands = sorted((ROOT / "profiles").glob(f"*pmc_traffic_c{config}.json"))
         if not cands:
             return None
         p = cands[-1]
@@ -122,8 +196,19 @@ def latest_pmc(path_arg):
         return None
 
 
+def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, seed0=1234):
+    import torch
+    torch.manual_seed(seed0)
+    engines = [sgmm.DRLEngine(pop_size=P_glob, phi=phi, tick_size=tick, fee_rate=0.0, use_arl=spec["arl"],
+                              save_dir=save_dir, hidden_dim=spec["H"], rng="device", seed=seed0 + 17 * k,
+                              val_mode="fused", sync_every=10**9, verbose=False, use_graph=use_graph, dist=dist)
+               for k, (phi, tick, _) in enumerate(spec["pops"])]
+    return sgmm.MultiDRLEngine(engines)
+
+
 def main():
     args = parse()
+    spec = workload_spec(args)
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -132,9 +217,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args)  # before the GPU is initialised (fork Pool)
+        cpu = cpu_baseline(spec, args.cpu_episodes)  # before the GPU is initialised (fork Pool)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
 
@@ -144,20 +228,23 @@ def main():
     import sgmm_pkg
     sgmm = sgmm_pkg.load()
     from sgmm_amd import _lib
+    from sgmm_amd.shard import shard_capacity
 
-    train, val, stats = workload(args)
-    P, H, T = args.pop, args.hidden, args.ticks
+    P, H, T, Tv = spec["P"], spec["H"], spec["T"], spec["Tv"]
+    P_glob = P * world if spec["scaling"] == "weak" else P
+    K = len(spec["pops"])
+    data = bundles(spec)
+    tr = [data[a][0] for _, _, a in spec["pops"]]
+    va = [data[a][1] for _, _, a in spec["pops"]]
+    st = [data[a][2] for _, _, a in spec["pops"]]
 
     def barrier():
         if world > 1:
             dist.barrier()
 
     tmp = tempfile.mkdtemp(prefix="sgmm_bench_")
-    eng = sgmm.DRLEngine(pop_size=P * world, phi=args.phi, tick_size=0.001, fee_rate=0.0,
-                         use_arl=False, save_dir=tmp, hidden_dim=H, rng="device", seed=1234,
-                         val_mode="fused", sync_every=10**9, verbose=False,
-                         use_graph=not args.no_graph)
-    sess = eng.session(train, val, stats, generations=args.warmup + args.steps)
+    eng = make_engine(sgmm, spec, P_glob, tmp, None, not args.no_graph)
+    sess = eng.session(tr, va, st, generations=args.warmup + args.steps)
     sess.steps(0, args.warmup)
     sess.capture()  # graphs recorded (not run) before the timed region
     torch.cuda.synchronize()
@@ -173,18 +260,17 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    _, hist = sess.finish()
+    res = sess.finish()
     ms_per_step = dt / args.steps * 1e3
-    value = world * P * T * args.steps / dt
+    value = K * P_glob * T * args.steps / dt
 
-    # per-kernel durations: eager generations of the same workload; the library
-    # hands each profiled kernel a pair of HIP events recorded by its own dispatch
-    # on the launch stream (hipExtLaunchKernel, sgmm_profile_*); graph replays
-    # launch the identical kernels
-    peng = sgmm.DRLEngine(pop_size=P, phi=args.phi, tick_size=0.001, use_arl=False, save_dir=tmp,
-                          hidden_dim=H, rng="device", seed=99, val_mode="fused", sync_every=10**9,
-                          verbose=False, use_graph=False, dist=False)
-    psess = peng.session(train, val, stats, generations=args.profile_steps + 2)
+    # per-kernel durations: eager generations of this rank's shard; the library
+    # hands each profiled kernel a pair of HIP events recorded by its own
+    # dispatch on the launch stream (hipExtLaunchKernel, sgmm_profile_*); graph
+    # replays launch the identical kernels
+    n_rank = shard_capacity(P_glob, world)
+    peng = make_engine(sgmm, spec, n_rank, tmp, False, False, seed0=99)
+    psess = peng.session(tr, va, st, generations=args.profile_steps + 2)
     psess.step(0)
     psess.step(1)
     torch.cuda.synchronize()
@@ -200,23 +286,23 @@ def main():
     gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, args.profile_steps)
 
     # roofline of the policy-table kernel (the FP32 compute kernel of the path)
-    steps_per_launch = P * (T + args.val_ticks)  # fused validation: train + val episodes
+    steps_per_launch = K * n_rank * (T + Tv)  # fused validation: train + validation episodes
     fl = flop_per_step(H)
     tab = kernels.get("policy_table")
-    pmc = latest_pmc(args.pmc)
+    pmc = latest_pmc(args.pmc, args.config)
     roofline = None
     if tab:
         achieved = steps_per_launch * fl / (tab["avg_us"] * 1e-6) / 1e12
         traffic = None
         if pmc and pmc.get("kernels", {}).get("policy_table"):
             traffic = pmc["kernels"]["policy_table"].get("hbm_bytes_per_launch")
-        roofline = {"bound": "mfma", "pipe": "fp32 VALU (gfx950 f32 MFMA peak == f32 VALU peak)",
-                    "kernel": "k_policy_table", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+        roofline = {"bound": "mfma", "pipe": "fp32 (gfx950 f32 MFMA peak == f32 VALU peak)",
+                    "kernel": "k_policy_table_mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-                    "algorithmic": {"flop_per_env_step": fl,
-                                    "env_steps_per_launch": steps_per_launch,
-                                    "note": "algorithmic = one policy forward per env-step; the table "
-                                            "kernel evaluates all 5 inventory states (5x this work)"},
+                    "algorithmic": {"flop_per_env_step": fl, "env_steps_per_launch": steps_per_launch,
+                                    "note": "algorithmic = one policy forward per env-step (train + validation "
+                                            "ticks of one launch); the table kernel evaluates every inventory "
+                                            "state (5x this work)"},
                     "avg_launch_us": tab["avg_us"]}
         if traffic:
             gbps = traffic / (tab["avg_us"] * 1e-6) / 1e9
@@ -229,13 +315,12 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": spec["scaling"], "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
-            "config": {"workload": "BASELINE config 2: GA generation, population 64/GPU, "
-                                   "TradingPolicy 3->16->16->2, synthetic 510300.SH ticks "
-                                   f"({T} train + {args.val_ticks} fused validation), no adversary",
-                       "population_per_gpu": P, "global_population": P * world, "hidden": H,
-                       "ticks_train": T, "ticks_val": args.val_ticks, "phi": args.phi,
+            "config": {"workload": describe(spec, world, P_glob), "config_id": args.config,
+                       "populations": K, "population_global": P_glob, "population_per_gpu": n_rank,
+                       "phis": [p for p, _, _ in spec["pops"]], "hidden": H, "ticks_train": T, "ticks_val": Tv,
+                       "adversary": spec["arl"], "val_mode": "fused",
                        "parallelism": f"population shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
                        "hip_graph": bool(sess.use_graph)},
             "generations_per_s": gens_per_s,
@@ -245,7 +330,7 @@ def main():
             "kernels": kernels,
             "dominant_kernel": dominant,
             "gen_kernel_time_us": gen_kernel_us,
-            "final_train_f": float(hist["train_f"][-1]) if hist["train_f"] else None,
+            "final_train_f": [float(h["train_f"][-1]) for _, h in res],
         }
         print(json.dumps(out))
     if world > 1:

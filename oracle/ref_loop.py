@@ -97,25 +97,62 @@ def _worker_init():
 
 def _run_one(i):
     mm, adv, bundle, phi, tick, fee, stats, hidden = _POOL_ARGS
-    return episode(mm[i], None if adv is None else adv[i], bundle, phi, tick, fee, stats, hidden)
+    ph = phi[i] if np.ndim(phi) else phi  # per-episode phi (a lambda sweep) or one for all
+    return episode(mm[i], None if adv is None else adv[i], bundle, ph, tick, fee, stats, hidden)
+
+
+def _noop(i):
+    return i
+
+
+class RefPool:
+    """A fork Pool of reference-loop workers (drl_engine.py:91), created and
+    warmed up OUTSIDE the timed region; ``map()`` times only the episodes.
+
+    ``phi`` may be one value or one per episode."""
+
+    def __init__(self, mm, adv, bundle, phi, tick, fee, stats, hidden=32, workers=1):
+        import multiprocessing as mp
+        global _POOL_ARGS
+        self.workers = int(workers)
+        _POOL_ARGS = (mm, adv, bundle, phi, tick, fee, stats, hidden)
+        torch.set_num_threads(1)
+        self.n = len(mm)
+        self.pool = None
+        if self.workers > 1:
+            self.pool = mp.get_context("fork").Pool(processes=self.workers, initializer=_worker_init)
+            self.pool.map(_noop, range(4 * self.workers), chunksize=1)  # every worker forked and running
+
+    def map(self):
+        """(fitness list, trades list, wall seconds of the episodes only)."""
+        t0 = time.perf_counter()
+        if self.pool is None:
+            res = [_run_one(i) for i in range(self.n)]
+        else:
+            res = self.pool.map(_run_one, range(self.n), chunksize=1)
+        dt = time.perf_counter() - t0
+        return [r[0] for r in res], [r[1] for r in res], dt
+
+    def close(self):
+        global _POOL_ARGS
+        if self.pool is not None:
+            self.pool.close()
+            self.pool.join()
+        _POOL_ARGS = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def population(mm, adv, bundle, phi, tick, fee, stats, hidden=32, workers=None):
     """Map episode() over a population with a fork Pool (drl_engine.py:91,115).
 
-    Returns (fitness list, trades list, wall seconds, workers used)."""
-    import multiprocessing as mp
-    global _POOL_ARGS
+    Returns (fitness list, trades list, wall seconds of the map, workers used);
+    pool start-up is not timed."""
     workers = int(workers or min(16, os.cpu_count() or 1))
-    _POOL_ARGS = (mm, adv, bundle, phi, tick, fee, stats, hidden)
-    torch.set_num_threads(1)
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    if workers <= 1:
-        res = [_run_one(i) for i in range(len(mm))]
-    else:
-        with ctx.Pool(processes=workers, initializer=_worker_init) as pool:
-            res = pool.map(_run_one, range(len(mm)), chunksize=1)
-    dt = time.perf_counter() - t0
-    _POOL_ARGS = None
-    return [r[0] for r in res], [r[1] for r in res], dt, workers
+    with RefPool(mm, adv, bundle, phi, tick, fee, stats, hidden, workers) as rp:
+        f, t, dt = rp.map()
+    return f, t, dt, workers
