@@ -296,8 +296,9 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
 // episode and of the table kernel per wave; slot 7 of a table wave holds
 // s_memrealtime at entry (a clock common to all XCDs)
 __device__ unsigned long long g_stamps[4096][16];
-__device__ unsigned long long g_tstamps[8192][8];
-__device__ unsigned int g_thwid[8192][2];  // HW_ID, XCC_ID of each table wave
+constexpr int kStampWaves = 1 << 16;
+__device__ unsigned long long g_tstamps[kStampWaves][8];
+__device__ unsigned int g_thwid[kStampWaves][2];  // HW_ID, XCC_ID of each table wave
 #define SGMM_STAMP(e, k)                                                           \
     do {                                                                           \
         unsigned long long t_;                                                     \
@@ -309,17 +310,17 @@ __device__ unsigned int g_thwid[8192][2];  // HW_ID, XCC_ID of each table wave
         unsigned long long t_;                                                     \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" \
                      : "=s"(t_) : "v"(dep) : "memory");                             \
-        if ((threadIdx.x & 63) == 0 && (w) < 8192) g_tstamps[w][k] = t_;           \
+        if ((threadIdx.x & 63) == 0 && (w) < kStampWaves) g_tstamps[w][k] = t_;    \
     } while (0)
 #define SGMM_TSTAMP_REAL(w, k)                                                         \
     do {                                                                               \
         unsigned long long t_;                                                         \
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-        if ((threadIdx.x & 63) == 0 && (w) < 8192) g_tstamps[w][k] = t_;               \
+        if ((threadIdx.x & 63) == 0 && (w) < kStampWaves) g_tstamps[w][k] = t_;        \
         unsigned h_, x_;                                                               \
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" \
                      : "=s"(h_), "=s"(x_));                                            \
-        if ((threadIdx.x & 63) == 0 && (w) < 8192) { g_thwid[w][0] = h_; g_thwid[w][1] = x_; } \
+        if ((threadIdx.x & 63) == 0 && (w) < kStampWaves) { g_thwid[w][0] = h_; g_thwid[w][1] = x_; } \
     } while (0)
 #else
 #define SGMM_STAMP(e, k) \
@@ -576,6 +577,473 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     SGMM_TSTAMP(wslot, 5, 0);
     SGMM_TSTAMP_REAL(wslot, 6);
 #endif
+}
+
+// ------------------------------------------------------------------ table v3: one state per MFMA stream
+// Same outputs and arithmetic as k_policy_table_mfma (!ARL), re-scheduled so
+// the matrix pipe never waits for the vector work of the state before it.
+// Two accumulator sets alternate between the inventory states; region r
+// (one per state, fenced by sched_barrier) issues
+//   MFMA:  layer 1 + layer 2 of state r+1 into set (r+1)&1 (pure registers),
+//   VALU:  relu + LDS transpose of state r (set r&1), layer 3 of state r and
+//          its FPT step (fp64), the transition byte and the reward staging,
+// so one wave carries both pipes; the vector work of a region (~200 issue
+// slots) fits in the 64 MFMA gaps (24 free cycles each, MI355X_MICROARCH.md
+// cycle constants).  Every lane computes every state (padded lanes read a
+// clamped tick and are masked out of the maps afterwards), so a region is a
+// single basic block.  Packed f32 FMAs are avoided beside the MFMAs (a
+// v_pk_fma_f32 there costs ~22 cycles more than two v_fma_f32).
+template <int H, int NSI, int MODE>
+__global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
+    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
+    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
+    double* __restrict__ rew) {
+    static_assert(H % 16 == 0 && H <= 32, "v3 table: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16;   // 16-neuron row tiles of layer 2
+    constexpr int KS = H / 4;    // k-steps (4 per MFMA)
+    constexpr int HP = H + 4;    // LDS row pitch (floats) of the transposed activations
+    const int e = blockIdx.y;
+    const int32_t T = ep.len[e];
+    const int wv = threadIdx.x >> 6;
+    const int chunk = blockIdx.x * 4 + wv;
+    const int32_t t0 = chunk * kChunk;
+    if (blockIdx.x * 4 * kChunk >= T) return;  // block-uniform
+    const int lane = threadIdx.x & (kWave - 1), grp = lane >> 4, col = lane & 15;
+    const int64_t tb = ep.tick_off[e];
+    // tick data requested before the genome staging so the loads overlap it
+    // (indices clamped into the episode: padded samples are discarded)
+    float xs0[4], xs1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t ti = tb + min(t0 + 16 * q + col, T - 1);
+        xs0[q] = tk.s1n[ti];
+        xs1[q] = tk.s2n[ti];
+    }
+    const int64_t tix = tb + min(t0 + lane, T - 1);
+    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
+    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
+    __shared__ __attribute__((aligned(16))) float gsm[L::N];
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __syncthreads();
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H];  // (W3[0][j], W3[1][j]) pairs
+    if (threadIdx.x < 2 * H) w3i[threadIdx.x] = gsm[L::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
+    __syncthreads();
+    if (t0 >= T) return;  // wave-uniform; no block barriers below
+#ifdef SGMM_STAMPS
+    // slots: 7 realtime at entry, 0 start, 1 weights + layer 1 of state 0,
+    // 2 states done, 3 map scan, 4 end, 5 / 6 summed MFMA / vector blocks
+    const int wslot = e * (int)(gridDim.x * 4) + chunk;
+    unsigned long long st_m = 0, st_v = 0, st_a, st_b;
+#define SGMM_V3T(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+#endif
+    SGMM_TSTAMP_REAL(wslot, 7);
+    SGMM_TSTAMP(wslot, 0, 0);
+    const sgmm_env_params p = params[ep.param[e]];
+    const float* g = gsm;
+    __shared__ __attribute__((aligned(16))) float hb_s[4][kWave * HP];
+    float* hb = hb_s[wv];
+    __shared__ double rl_s[4][NSI][kWave];  // [state][lane] rewards for the path planes
+    double* rl = &rl_s[wv][0][0];
+
+    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
+    f32x4 b2c[NT];      // C of layer 2: neurons 16rt + 4grp + r
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * grp + r];
+    }
+    float w1s[KS];      // W1[k][2], k = 4i + grp
+    float pre[4][KS];   // b1[k] + W1[k][0] s1n + W1[k][1] s2n of sample 16q + col
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const int k = 4 * i + grp;
+        const float a0 = g[L::W1 + 3 * k], a1 = g[L::W1 + 3 * k + 1], bb = g[L::B1 + k];
+        w1s[i] = g[L::W1 + 3 * k + 2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(a1, xs1[q], __builtin_fmaf(a0, xs0[q], bb));
+    }
+    const float b30 = g[L::B3], b31 = g[L::B3 + 1];
+
+    f32x4 acc[MODE == 0 ? 2 : 1][4][NT];
+    uint64_t map = kIdentityMap;
+    uint32_t traded = 0;
+    auto layer12 = [&](int si, int b) {  // layer 1 (VALU) + layer 2 (MFMA) of state si into set b
+        const float x2 = (float)((double)(inv_min + si) / 2.0);
+#pragma unroll
+        for (int i = 0; i < KS; ++i)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt)
+                    acc[b][q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1,
+                                                                         i == 0 ? b2c[rt] : acc[b][q][rt], 0, 0, 0);
+            }
+    };
+    auto transpose = [&](int b) {  // relu(H2) of set b -> LDS [sample][neuron]
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = relu(acc[b][q][rt][r]);
+                *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+            }
+    };
+    auto layer3_env = [&](int si) {  // layer 3 of this lane's tick, then its FPT step from state si
+        float o0 = b30, o1 = b31;
+#pragma unroll
+        for (int j4 = 0; j4 < H / 4; ++j4) {
+            const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(&w3i[2 * (4 * j4 + 2 * r2)]);
+                o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+            }
+        }
+        const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+        const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+        const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
+        const bool live = si < nsi;  // states past the caps keep the identity byte
+        const uint64_t to = live ? (uint64_t)(si + so.fill_buy - so.fill_sell) : (uint64_t)si;
+        map = (map & ~(0xFFull << (8 * si))) | (to << (8 * si));
+        traded |= (uint32_t)(live && (so.fill_buy | so.fill_sell)) << si;
+        rl[si * kWave + lane] = so.reward;
+    };
+    if constexpr (MODE == 0) {
+        layer12(0, 0);
+#pragma unroll
+        for (int si = 0; si < NSI; ++si) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (si + 1 < NSI) layer12(si + 1, (si + 1) & 1);
+            transpose(si & 1);
+            layer3_env(si);
+        }
+    } else {
+        // one accumulator set; per state a vector block (transpose of state
+        // si, layer 1 of si+1, layer 3 + FPT step of si) and a pure MFMA block
+        // (layer 2 of si+1): f32 MFMAs and vector ops of ONE wave do not
+        // overlap on gfx950 (tools/mb/mb_mfma_valu.hip), so the blocks are
+        // kept apart and the overlap comes from the other waves of the SIMD
+        float h1[KS][4];
+        auto layer1 = [&](int si) {
+            const float x2 = (float)((double)(inv_min + si) / 2.0);
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) h1[i][q] = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+        };
+        auto layer2 = [&]() {
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int rt = 0; rt < NT; ++rt)
+                        acc[0][q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[i][q],
+                                                                             i == 0 ? b2c[rt] : acc[0][q][rt], 0, 0, 0);
+        };
+        layer1(0);
+        SGMM_TSTAMP(wslot, 1, h1[KS - 1][3] + pre[0][0] + w2f[0][0] + b2c[0][0]);
+#ifdef SGMM_STAMPS
+        SGMM_V3T(st_b);
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+        layer2();
+#pragma unroll
+        for (int si = 0; si < NSI; ++si) {
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef SGMM_STAMPS
+            SGMM_V3T(st_a);
+            st_m += st_a - st_b;
+#endif
+            transpose(0);
+            if (si + 1 < NSI) layer1(si + 1);
+            layer3_env(si);
+            __builtin_amdgcn_sched_barrier(0);
+#ifdef SGMM_STAMPS
+            SGMM_V3T(st_b);
+            st_v += st_b - st_a;
+#endif
+            if (si + 1 < NSI) layer2();
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    SGMM_TSTAMP(wslot, 2, map + traded);
+    const bool valid = t0 + lane < T;
+    if (!valid) {  // padded lanes: identity steps, no trades
+        map = kIdentityMap;
+        traded = 0;
+    }
+    const uint64_t inc = wave_map_scan(map);
+    uint64_t excl = shfl_up_u64(inc, 1);
+    if (lane == 0) excl = kIdentityMap;
+    SGMM_TSTAMP(wslot, 3, excl);
+    // path planes: plane s holds the reward along the chunk's path from start
+    // state s; per start state the path's trade count (8 bits each)
+    const int64_t row = ep.step_off[e] + t0 + lane;
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int s0 = 0; s0 < NSI; ++s0) {
+        if (s0 >= nsi) break;
+        const uint32_t st = map_get(excl, (uint32_t)s0);
+        if (valid) rew[s0 * ep.rs + row] = rl[st * kWave + lane];
+        cnt |= (uint64_t)__popcll(__ballot(valid && ((traded >> st) & 1u))) << (8 * s0);
+    }
+    if (lane == kWave - 1) {
+        const uint32_t ci = chunk_base(ep.step_off[e], e) + chunk;
+        cmaps[ci] = inc;
+        ctr[ci] = cnt;
+    }
+#ifdef SGMM_STAMPS
+    SGMM_TSTAMP(wslot, 4, 0);
+    if (lane == 0 && wslot < kStampWaves) {
+        g_tstamps[wslot][5] = st_m;
+        g_tstamps[wslot][6] = st_v;
+    }
+#undef SGMM_V3T
+#endif
+}
+
+// ------------------------------------------------------------------ frontier kernel
+// The table evaluates the policy for every inventory state of every tick,
+// because a chunk's start state is unknown until the scan.  But the paths
+// from the different start states merge within a few ticks (fills move the
+// inventory by +-1 against the caps): on the bench data a chunk's paths are at
+// 1.2 distinct states per tick on average, not 5.  So here one wave walks a
+// whole episode, lane = one chunk of CL = frontier_len(T) consecutive ticks
+// (at most 64 chunks), and at each tick evaluates only the states its paths
+// are currently in (the "frontier"):
+//   per tick: slot k = the k-th frontier state of every lane; the layer-2
+//   MFMAs run per 16-lane tile only while one of its lanes has a k-th state
+//   (samples = the 64 lanes' chunks at the same tick offset); layer 3, the
+//   FPT step and the frontier update run per lane.
+// Per chunk it writes what the scan needs: the chunk map (byte s = end state of
+// the path from start state s), the trade count along each path (u32), the
+// path rewards (plane s, row = tick) -- and once every tracked path has merged
+// (tick offset kc) only plane p0 (the lowest start state), so the planes cost
+// ~1.3 rows per tick instead of one per state.  Chunk 0 starts at inventory 0;
+// the other chunks track every state in [inv_min, inv_max].  Arithmetic per
+// (tick, state) is the table's (same MFMA chains, same fp64 step), so every
+// output bit is the table's.
+constexpr int kFrontierSlots = 64;   // chunks (lanes) per episode
+__host__ __device__ __forceinline__ int frontier_len(int T) {
+    const int c = (T + kFrontierSlots - 1) / kFrontierSlots;
+    return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
+}
+
+template <int H, int NSI>
+__global__ __launch_bounds__(kWave) void k_policy_frontier(
+    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
+    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ cmaps, uint32_t* __restrict__ ctr32,
+    uint32_t* __restrict__ kinfo, double* __restrict__ rew) {
+    static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16, KS = H / 4, HP = H + 4;
+    const int e = blockIdx.x;
+    const int32_t T = ep.len[e];
+    if (T <= 0) return;  // block-uniform
+    const int CL = frontier_len(T);
+    const int nch = (T + CL - 1) / CL;
+    const int lane = threadIdx.x, grp = lane >> 4, col = lane & 15;
+    const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
+    const int t0 = lane * CL;                          // this lane's chunk
+    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
+
+    __shared__ __attribute__((aligned(16))) float gsm[L::N];
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H];   // (W3[0][j], W3[1][j])
+    __shared__ __attribute__((aligned(16))) float l1w[H][4];    // (W1[k][0], W1[k][1], b1[k], W1[k][2])
+    __shared__ __attribute__((aligned(16))) float hb[kWave * HP];
+    __shared__ double rl[NSI][kWave];
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __syncthreads();
+    if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
+    if (lane < H) {
+        l1w[lane][0] = gsm[L::W1 + 3 * lane];
+        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
+        l1w[lane][2] = gsm[L::B1 + lane];
+        l1w[lane][3] = gsm[L::W1 + 3 * lane + 2];
+    }
+    __syncthreads();
+    const sgmm_env_params p = params[ep.param[e]];
+    const float* g = gsm;
+    float w2f[NT][KS];
+    f32x4 b2c[NT];
+    float w1s[KS];
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * grp + r];
+    }
+#pragma unroll
+    for (int i = 0; i < KS; ++i) w1s[i] = l1w[4 * i + grp][3];
+    const float b30 = g[L::B3], b31 = g[L::B3 + 1];
+
+    // per-lane path bookkeeping: byte s of cur = the state of the path that
+    // started the chunk in state s (tracked starts: bits of sset)
+    const uint32_t all = (1u << nsi) - 1u;
+    const uint32_t sset = lane >= nch ? 0u : (lane == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
+    uint64_t cur = kIdentityMap;
+    uint32_t cnt[NSI];
+#pragma unroll
+    for (int s = 0; s < NSI; ++s) cnt[s] = 0;
+    bool merged = __builtin_popcount(sset) <= 1;
+    int kc = merged ? 0 : CL;
+    // the next tick's inputs, loaded one tick ahead
+    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
+    int64_t ti = tick_of(0);
+    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];
+    double nmid = tk.mid_next[ti], nask = tk.best_ask[ti], nbid = tk.best_bid[ti];
+    double nbmax = tk.buy_max[ti], nsmin = tk.sell_min[ti];
+    f32x4 acc[4][NT];
+#pragma unroll 1
+    for (int tt = 0; tt < CL; ++tt) {
+        const bool act = tt < ntl;
+        const float s1 = ns1, s2 = ns2;
+        const double tmid = nmid, task = nask, tbid = nbid, tbmax = nbmax, tsmin = nsmin;
+        ti = tick_of(tt + 1);
+        ns1 = tk.s1n[ti];
+        ns2 = tk.s2n[ti];
+        nmid = tk.mid_next[ti];
+        nask = tk.best_ask[ti];
+        nbid = tk.best_bid[ti];
+        nbmax = tk.buy_max[ti];
+        nsmin = tk.sell_min[ti];
+        // frontier: the distinct current states of the tracked paths
+        uint32_t fmask = 0;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s)
+            if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
+        if (!act) fmask = 0;
+        // slots per 16-lane tile: the most frontier states of any of its lanes
+        int ns = __builtin_popcount(fmask);
+        ns = max(ns, __shfl_xor(ns, 1, kWave));
+        ns = max(ns, __shfl_xor(ns, 2, kWave));
+        ns = max(ns, __shfl_xor(ns, 4, kWave));
+        ns = max(ns, __shfl_xor(ns, 8, kWave));
+        int tsl[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) tsl[q] = __builtin_amdgcn_readlane(ns, 16 * q);
+        const int nslot = max(max(tsl[0], tsl[1]), max(tsl[2], tsl[3]));
+        // the weights stay in LDS (an opaque offset per tick keeps the compiler
+        // from hoisting them into ~90 registers across the tick loop)
+        int lofs = 0;
+        asm volatile("" : "+s"(lofs));
+        // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
+        float pre[4][KS];
+        {
+            float xs0[4], xs1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xs0[q] = __shfl(s1, 16 * q + col, kWave);
+                xs1[q] = __shfl(s2, 16 * q + col, kWave);
+            }
+#pragma unroll
+            for (int i = 0; i < KS; ++i) {
+                const f32x4 w = *reinterpret_cast<const f32x4*>(&l1w[4 * i + grp][0] + lofs);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
+            }
+        }
+        uint32_t rem = fmask;
+        uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
+        uint32_t trm = 0;                 // bit f: a fill from frontier state f
+#pragma unroll 1
+        for (int k = 0; k < nslot; ++k) {
+            int sofs = 0;
+            asm volatile("" : "+s"(sofs));
+            const bool has = rem != 0u;
+            const uint32_t f = has ? (uint32_t)__builtin_ctz(rem) : 0u;
+            rem &= rem - 1u;
+            const float x2own = (float)((double)(inv_min + (int)f) / 2.0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (k >= tsl[q]) continue;  // wave-uniform: no lane of tile q has a k-th state
+                const float x2 = __shfl(x2own, 16 * q + col, kWave);
+#pragma unroll
+                for (int i = 0; i < KS; ++i) {
+                    const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+#pragma unroll
+                    for (int rt = 0; rt < NT; ++rt)
+                        acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, i == 0 ? b2c[rt] : acc[q][rt],
+                                                                          0, 0, 0);
+                }
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+                }
+            }
+            float o0 = b30, o1 = b31;
+#pragma unroll
+            for (int j4 = 0; j4 < H / 4; ++j4) {
+                const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+                for (int r2 = 0; r2 < 2; ++r2) {
+                    const f32x4 w = *reinterpret_cast<const f32x4*>(&w3i[2 * (4 * j4 + 2 * r2)] + sofs);
+                    o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                    o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                    o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                    o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                }
+            }
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
+            if (has) {
+                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
+                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
+                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
+                rl[f][lane] = so1.reward;
+            }
+        }
+        // the tick's rewards along the tracked paths; once they have merged only plane p0
+        if (act) {
+            const int64_t row = so + t0 + tt;
+#pragma unroll
+            for (int s = 0; s < NSI; ++s) {
+                if (!((sset >> s) & 1u)) continue;
+                const uint32_t st = map_get(cur, (uint32_t)s);
+                if (!merged || (uint32_t)s == p0) rew[s * ep.rs + row] = rl[st][lane];
+                cnt[s] += (trm >> st) & 1u;
+            }
+            cur = map_then(cur, stepmap);
+            if (!merged) {
+                uint32_t fm = 0;
+#pragma unroll
+                for (int s = 0; s < NSI; ++s)
+                    if ((sset >> s) & 1u) fm |= 1u << map_get(cur, (uint32_t)s);
+                if (__builtin_popcount(fm) <= 1) {
+                    merged = true;
+                    kc = tt + 1;
+                }
+            }
+        }
+    }
+    if (lane < nch) {
+        // untracked start states keep the identity byte (never on the episode's path)
+        uint64_t cm = kIdentityMap;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s)
+            if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
+        const int64_t ci = (int64_t)e * kFrontierSlots + lane;
+        cmaps[ci] = cm;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = cnt[s];
+        kinfo[ci] = (uint32_t)kc | (p0 << 29);
+    }
 }
 
 // ------------------------------------------------------------------ exact ordered sum
@@ -983,23 +1451,27 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
 //   2. every thread: the rewards of its 4 ticks from the path plane of their
 //      chunk's start state (one coalesced row per chunk) -> LDS;
 //   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
-template <int NSM, int NT>
+template <int NSM, int NT, bool FR>
 __global__ __launch_bounds__(NT) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
     const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
-    const double* __restrict__ rew, double* __restrict__ fitness,
+    const uint32_t* __restrict__ kinfo, const double* __restrict__ rew, double* __restrict__ fitness,
     int32_t* __restrict__ trades_out, StepArgs step) {
+    // FR: the frontier kernel's chunks (frontier_len(T) ticks, at most 64 per
+    // episode, slots e * 64 + c, u32 trade counts, kinfo = merge tick | p0 << 29)
     constexpr int kWin = NT * kSumTpt;
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);  // [kWin]
     __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[kMaxLen / kChunk];
+    __shared__ uint8_t start[FR ? kFrontierSlots : kMaxLen / kChunk];
+    __shared__ uint32_t kin[FR ? kFrontierSlots : 1];
     __shared__ int red_trades;
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
-    const int nch = (T + kChunk - 1) / kChunk;
+    const int CL = FR ? frontier_len(T) : kChunk;
+    const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
-    const uint32_t cb = chunk_base(so, e);
+    const int64_t cb = FR ? (int64_t)e * kFrontierSlots : (int64_t)chunk_base(so, e);
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
     SGMM_STAMP(e, 0);
     if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
@@ -1008,13 +1480,20 @@ __global__ __launch_bounds__(NT) void k_path_scan(
         for (int c0 = 0; c0 < nch; c0 += kWave) {
             const int c = c0 + lane;
             const uint64_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
-            const uint64_t k = c < nch ? ctr[cb + c] : 0;
+            const uint64_t k = (!FR && c < nch) ? ctr[cb + c] : 0;
             const uint64_t inc = wave_map_scan(m);
             uint64_t excl = shfl_up_u64(inc, 1);
             if (lane == 0) excl = kIdentityMap;
             const uint32_t st = map_get(excl, s);
             if (c < nch) start[c] = (uint8_t)st;
-            tr += (int)((k >> (8 * st)) & 0xFFu);
+            if (FR) {
+                if (c < nch) {
+                    tr += (int)reinterpret_cast<const uint32_t*>(ctr)[(cb + c) * 8 + st];
+                    kin[c] = kinfo[cb + c];
+                }
+            } else {
+                tr += (int)((k >> (8 * st)) & 0xFFu);
+            }
             s = map_get(readlane64(inc, kWave - 1), s);
         }
 #pragma unroll
@@ -1027,11 +1506,23 @@ __global__ __launch_bounds__(NT) void k_path_scan(
     for (int w0 = 0; w0 < T; w0 += kWin) {
         const int n = min(kWin, T - w0);
         const int i0 = tid * kSumTpt;
-        if (i0 < n) {  // 4 ticks of one chunk (kChunk % kSumTpt == 0)
-            const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
+        if (i0 < n) {  // 4 ticks of one chunk (CL % kSumTpt == 0)
             double r[kSumTpt];
+            if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
+                const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
+                const uint32_t ki = kin[c];
+                const int kc = (int)(ki & 0x1FFFFFFFu);
+                const int64_t pst = start[c], pp0 = ki >> 29;
 #pragma unroll
-            for (int j = 0; j < kSumTpt; ++j) r[j] = src[min(j, n - 1 - i0)];
+                for (int j = 0; j < kSumTpt; ++j) {
+                    const int jj = min(j, n - 1 - i0);
+                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + so + w0 + i0 + jj];
+                }
+            } else {
+                const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
+#pragma unroll
+                for (int j = 0; j < kSumTpt; ++j) r[j] = src[min(j, n - 1 - i0)];
+            }
 #pragma unroll
             for (int j = 0; j < kSumTpt; ++j)
                 if (i0 + j < n) sel[i0 + j] = r[j];
@@ -1321,8 +1812,7 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     SGMM_REQUIRE(tk && eps && params && mm, "null ticks/episodes/params/genomes");
     SGMM_REQUIRE(eps->n >= 0, "n episodes < 0");
     SGMM_REQUIRE(supported_hidden(hidden), "hidden=%d unsupported (8,16,32,64)", hidden);
-    SGMM_REQUIRE(eps->max_len >= 0 && eps->max_len <= kMaxLen, "max_len=%d out of [0,%d]",
-                 eps->max_len, kMaxLen);
+    SGMM_REQUIRE(eps->max_len >= 0, "max_len=%d < 0", eps->max_len);
     SGMM_REQUIRE(eps->inv_min <= 0 && eps->inv_max >= 0 && eps->inv_max - eps->inv_min + 1 <= 8,
                  "inventory range [%d,%d] must contain 0 and span <= 8 values", eps->inv_min,
                  eps->inv_max);
@@ -1349,7 +1839,10 @@ static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 // (A/B measurements and as an independent cross-check in the tests).
 static int table_path() {
     const char* e = std::getenv("SGMM_TABLE_PATH");
-    return (e && std::strcmp(e, "valu") == 0) ? 1 : 0;
+    if (e && std::strcmp(e, "valu") == 0) return 1;
+    if (e && std::strcmp(e, "v2") == 0) return 2;  // k_policy_table_mfma without the v3 schedule
+    if (e && std::strcmp(e, "v3i") == 0) return 3;  // v3 with two accumulator sets, blocks interleaved
+    return 0;
 }
 
 }  // namespace sgmm
@@ -1376,9 +1869,17 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 //                 slots) | f64 path planes rew[n_states][rs] (rs = total_steps
 //                 rounded up to 32)
 //   adversary:    u64 fills[total_steps] | f64 rew[total_steps][n_states]
+//   (frontier kernel: cmaps / ctr hold u64 maps / u32[8] trade counts at slots
+//   e * 64 + c, then u32 kinfo[n * 64]; the sections are sized for both)
 static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
-static size_t ws_cmaps(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint64_t)); }
-static size_t ws_ctr(int32_t n, int64_t steps) { return align256(n_chunk_slots(n, steps) * sizeof(uint64_t)); }
+static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierSlots; }
+static size_t ws_cmaps(int32_t n, int64_t steps) {
+    return align256(std::max(n_chunk_slots(n, steps), n_frontier_slots(n)) * sizeof(uint64_t));
+}
+static size_t ws_ctr(int32_t n, int64_t steps) {
+    return align256(std::max(n_chunk_slots(n, steps) * sizeof(uint64_t), n_frontier_slots(n) * 8 * sizeof(uint32_t)));
+}
+static size_t ws_kinfo(int32_t n) { return align256(n_frontier_slots(n) * sizeof(uint32_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
@@ -1386,8 +1887,22 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
     if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
     if (n_states > 8)  // adversary: rew[row * n_states + state]
         return ws_fills(total_steps) + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
-    return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) +
+    return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
            (size_t)rew_stride(total_steps) * (size_t)n_states * sizeof(double);
+}
+
+// Frontier kernel or table: the frontier kernel does ~1/3 of the table's
+// matrix work but walks each episode serially (one wave per episode), so it
+// needs many episodes to fill the chip; it is also the only path for episodes
+// longer than kMaxLen.  SGMM_TABLE_PATH=frontier / table forces either.
+constexpr int kFrontierMinEps = 2048;
+static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
+    if (arl || (hidden != 16 && hidden != 32)) return false;
+    if (eps->max_len > kMaxLen) return true;
+    const char* v = std::getenv("SGMM_TABLE_PATH");
+    if (v && std::strcmp(v, "frontier") == 0) return true;
+    if (v && *v) return false;
+    return eps->n >= kFrontierMinEps;
 }
 
 template <int H>
@@ -1397,6 +1912,23 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
                               uint64_t* ctr, uint64_t* cmaps, uint64_t* fills, double* rew) {
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
+    if constexpr (H <= 32) {
+        const int tp = table_path();
+        if (!arl && (tp == 0 || tp == 3)) {
+#define SGMM_TABLE_V3(NSI_, MODE_)                                                                       \
+    SGMM_LAUNCH((k_policy_table_v3<H, NSI_, MODE_>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, \
+                ctr, cmaps, rew)
+            if (tp == 3) {
+                if (nsi <= 5) SGMM_TABLE_V3(5, 0);
+                else SGMM_TABLE_V3(8, 0);
+            } else {
+                if (nsi <= 5) SGMM_TABLE_V3(5, 1);
+                else SGMM_TABLE_V3(8, 1);
+            }
+#undef SGMM_TABLE_V3
+            return;
+        }
+    }
 #define SGMM_TABLE_MFMA(NSI_, ARL_)                                                               \
     SGMM_LAUNCH((k_policy_table_mfma<H, NSI_, ARL_>), grid, block, 0, s, tk, ep, params,  \
                        src, inv_min, nsi, ctr, cmaps, fills, rew)
@@ -1443,20 +1975,20 @@ static int scan_threads(int64_t n) {
     return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : 256);
 }
 
-template <int NSM>
+template <int NSM, bool FR>
 static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
                              const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
-                             const uint64_t* ctr, const double* rew, double* fitness, int32_t* trades,
-                             const StepArgs& step) {
+                             const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
+                             int32_t* trades, const StepArgs& step) {
     if (nt == kScanThreads)
-        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
-                    cmaps, ctr, rew, fitness, trades, step);
+        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, kinfo, rew, fitness, trades, step);
     else if (nt == 512)
-        SGMM_LAUNCH((k_path_scan<NSM, 512>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    rew, fitness, trades, step);
+        SGMM_LAUNCH((k_path_scan<NSM, 512, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    kinfo, rew, fitness, trades, step);
     else
-        SGMM_LAUNCH((k_path_scan<NSM, 256>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    rew, fitness, trades, step);
+        SGMM_LAUNCH((k_path_scan<NSM, 256, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    kinfo, rew, fitness, trades, step);
 }
 
 // table + path scan (+ the generation tail when step.st) for one batch
@@ -1477,18 +2009,38 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     uint64_t* ctr = nullptr;
     uint64_t* cmaps = nullptr;
     uint64_t* fills = nullptr;
+    uint32_t* kinfo = nullptr;
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
         rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
     } else {
+        const size_t a = ws_cmaps(eps->n, eps->total_steps), b = ws_ctr(eps->n, eps->total_steps);
         cmaps = reinterpret_cast<uint64_t*>(w);
-        ctr = reinterpret_cast<uint64_t*>(w + ws_cmaps(eps->n, eps->total_steps));
-        rew = reinterpret_cast<double*>(w + ws_cmaps(eps->n, eps->total_steps) +
-                                        ws_ctr(eps->n, eps->total_steps));
+        ctr = reinterpret_cast<uint64_t*>(w + a);
+        kinfo = reinterpret_cast<uint32_t*>(w + a + b);
+        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n));
     }
     const EpArrays ep = ep_arrays(eps, arl);
-    if (eps->max_len > 0) {
+    const bool fr = use_frontier(arl, hidden, eps);
+    SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
+                 "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
+    if (fr && eps->max_len > 0) {
+        ProfScope prof("policy_table", s);
+        const dim3 grid(eps->n), block(kWave);
+#define SGMM_FRONTIER(H_, NSI_)                                                                            \
+    SGMM_LAUNCH((k_policy_frontier<H_, NSI_>), grid, block, 0, s, *ticks, ep, params, src, eps->inv_min, nsi, \
+                cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew)
+        if (hidden == 16) {
+            if (nsi <= 5) SGMM_FRONTIER(16, 5);
+            else SGMM_FRONTIER(16, 8);
+        } else {
+            if (nsi <= 5) SGMM_FRONTIER(32, 5);
+            else SGMM_FRONTIER(32, 8);
+        }
+#undef SGMM_FRONTIER
+        SGMM_LAUNCHED();
+    } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof("policy_table", s);
         const bool valu = table_path() == 1;
@@ -1525,12 +2077,20 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         const int nt = scan_threads(eps->n);
         size_t lds = (size_t)nt * kSumTpt * sizeof(double);
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
-        if (nsi <= 5)
-            launch_path_scan<5>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, rew, fitness,
-                                trades, step);
-        else
-            launch_path_scan<8>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, rew, fitness,
-                                trades, step);
+        if (fr) {
+            if (nsi <= 5)
+                launch_path_scan<5, true>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
+                                          fitness, trades, step);
+            else
+                launch_path_scan<8, true>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
+                                          fitness, trades, step);
+        } else if (nsi <= 5) {
+            launch_path_scan<5, false>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
+                                       fitness, trades, step);
+        } else {
+            launch_path_scan<8, false>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
+                                       fitness, trades, step);
+        }
     }
     SGMM_LAUNCHED();
     return SGMM_OK;
