@@ -1,0 +1,128 @@
+"""GPU parity of the frontier kernel (k_policy_frontier + the frontier path
+scan): one wave per episode, lane = one of <= 64 chunks, only the inventory
+states the chunk's paths occupy are evaluated, planes written once per tick
+after the paths merge.  Every result must equal the CPU oracle bit for bit --
+the same per-(tick, state) arithmetic as the table, a different schedule.
+Reference: Env/drl_engine.py:9-67 (evaluate_individual), Env/market_env.py:22-67.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import has_gpu
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not has_gpu(), reason="needs a HIP device")]
+
+DEV = torch.device("cuda:0")
+
+
+@pytest.fixture
+def frontier(monkeypatch):
+    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
+
+
+def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
+         n_threads=8):
+    from sgmm_amd import synthetic
+    lens = np.asarray(lens, np.int64)
+    P = len(lens)
+    T = int(lens.max()) if T is None else T
+    b = synthetic.bundle_510300(max(T, 1), seed=seed, nan_frac=nan_frac)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=sigma, seed=seed + 1)
+    i_max, i_min = caps
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    cfg = sgmm.EnvConfig(phi=phi, tick_size=0.001, fee_rate=fee, i_max=i_max, i_min=i_min)
+    params = sgmm.params_tensor([cfg], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
+                           inv_min=i_min, inv_max=i_max).to(DEV)
+    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,
+                                           np.zeros(P), lens, np.zeros(P),
+                                           [oracle.params(phi=phi, tick=0.001, fee=fee, i_max=i_max, i_min=i_min)],
+                                           n_threads=n_threads)
+    return fit.cpu().numpy(), trd.cpu().numpy(), want_f, want_t
+
+
+@pytest.mark.parametrize("H", [16, 32])
+def test_frontier_ragged_lengths(sgmm, oracle, frontier, H):
+    """Chunk lengths from 4 ticks (T <= 256) up: lengths around 4 * 64, the
+    chunk / window boundaries, a length not divisible by its chunk, 0 and 1."""
+    lens = [0, 1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 258, 1000, 4095, 4096, 4097, 4560, 9001]
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=41)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+    assert fit[0] == -50.0 and trd[0] == 0
+
+
+@pytest.mark.parametrize("caps", [(2, -2), (1, -1), (1, -3), (3, -4), (0, 0)],
+                         ids=["5states", "3states", "offcentre", "8states", "1state"])
+def test_frontier_inventory_ranges(sgmm, oracle, frontier, caps):
+    """Caps other than +-2: 1, 3, 5 (inventory 0 off-centre) and 8 states."""
+    fit, trd, wf, wt = _run(sgmm, oracle, [700, 2000, 3001, 64, 65], 16, seed=43, caps=caps, sigma=0.5)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
+def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
+    """NaN FPT bounds (no fill), fees, and a wide population (sigma 1: policies
+    that quote far away, so paths merge late or never)."""
+    fit, trd, wf, wt = _run(sgmm, oracle, [3600] * 12 + [720] * 12, 32, seed=45, nan_frac=0.05, sigma=1.0,
+                            fee=3e-5)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
+def test_frontier_default_selection_many_episodes(sgmm, oracle):
+    """From 2048 episodes on the frontier kernel is the default: 2100 ragged
+    episodes bit-exact against the oracle."""
+    lens = 300 + (np.arange(2100) * 37) % 900
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=47, sigma=0.3)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
+def test_frontier_lifts_the_episode_length_cap(sgmm, oracle, monkeypatch):
+    """Episodes longer than the table's 131072-tick cap run on the frontier
+    kernel (agent_trainer.py:74-77 concatenates days without a bound): a
+    300 000-tick episode bit-exact; forcing the table path fails cleanly."""
+    fit, trd, wf, wt = _run(sgmm, oracle, [300000, 131073, 5], 32, seed=49, sigma=0.1)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+    from sgmm_amd import synthetic
+    b = synthetic.bundle_510300(131073, seed=1)
+    st = synthetic.train_stats(b)
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.001, tick_size=0.001)], DEV)
+    eb = sgmm.EpisodeBatch([0], [ticks.segments[seg][0]], [131073], [0]).to(DEV)
+    adv = synthetic.population(1, 32, seed=2).to(DEV)
+    from sgmm_amd._lib import SgmmError
+    with pytest.raises(SgmmError, match="frontier"):  # the adversary path has no frontier kernel
+        sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, synthetic.population(1, 32, seed=3).to(DEV), 32, adv)
+
+
+def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
+    """DRLEngine (device RNG, fused validation) trains identically with the
+    frontier kernel and with the table: histories and final masters."""
+    from sgmm_amd import synthetic
+    tr = synthetic.bundle_510300(900, seed=51)
+    va = synthetic.bundle_510300(200, seed=52)
+    st = synthetic.train_stats(tr)
+    out = {}
+    for path in ("table", "frontier"):
+        monkeypatch.setenv("SGMM_TABLE_PATH", path)
+        torch.manual_seed(7)
+        eng = sgmm.DRLEngine(pop_size=40, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / path), hidden_dim=32,
+                             rng="device", seed=99, sync_every=4, verbose=False)
+        pol, hist = eng.train(tr, va, st, generations=10)
+        out[path] = (pol.get_weights().numpy(), hist)
+    (wa, ha), (wb, hb) = out["table"], out["frontier"]
+    for k in ha:
+        assert np.array_equal(np.array(ha[k], np.float64), np.array(hb[k], np.float64), equal_nan=True), k
+    assert np.array_equal(wa, wb)
