@@ -834,19 +834,22 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
 // (tick, state) is the table's (same MFMA chains, same fp64 step), so every
 // output bit is the table's.
 constexpr int kFrontierSlots = 64;   // chunks (lanes) per episode
+typedef __attribute__((address_space(3))) const float lds_cf;
+typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
 __host__ __device__ __forceinline__ int frontier_len(int T) {
     const int c = (T + kFrontierSlots - 1) / kFrontierSlots;
     return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
 }
 
 template <int H, int NSI>
-__global__ __launch_bounds__(kWave) void k_policy_frontier(
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
     int32_t inv_min, int32_t nsi, uint64_t* __restrict__ cmaps, uint32_t* __restrict__ ctr32,
     uint32_t* __restrict__ kinfo, double* __restrict__ rew) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
-    constexpr int NT = H / 16, KS = H / 4, HP = H + 4;
+    constexpr int NT = H / 16, KS = H / 4;
+    constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
@@ -857,36 +860,37 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
     const int t0 = lane * CL;                          // this lane's chunk
     const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
 
-    __shared__ __attribute__((aligned(16))) float gsm[L::N];
-    __shared__ __attribute__((aligned(16))) float w3i[2 * H];   // (W3[0][j], W3[1][j])
-    __shared__ __attribute__((aligned(16))) float l1w[H][4];    // (W1[k][0], W1[k][1], b1[k], W1[k][2])
-    __shared__ __attribute__((aligned(16))) float hb[kWave * HP];
-    __shared__ double rl[NSI][kWave];
+    // LDS (~9 KB per wave, so 3 waves per SIMD fit): the genome is staged in
+    // `big`, the weights the loop needs are copied out, then `big` holds the
+    // half-activation transpose buffer and the per-state rewards
+    constexpr int kBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
+    __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 4];  // (W3[0][j], W3[1][j]) pairs, then b3
+    __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
+    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
+    __shared__ __attribute__((aligned(16))) float b2s[H];
+    float* gsm = reinterpret_cast<float*>(big);
     stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
     __syncthreads();
     if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
+    if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
     if (lane < H) {
+        w1x[lane & 3][lane >> 2] = gsm[L::W1 + 3 * lane + 2];
         l1w[lane][0] = gsm[L::W1 + 3 * lane];
         l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
         l1w[lane][2] = gsm[L::B1 + lane];
         l1w[lane][3] = gsm[L::W1 + 3 * lane + 2];
+        b2s[lane] = gsm[L::B2 + lane];
     }
-    __syncthreads();
+    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+    __syncthreads();  // gsm is dead from here: big becomes hb + rl
+    float* hb = reinterpret_cast<float*>(big);                          // [64][HP]
+    double* rl = reinterpret_cast<double*>(big + kWave * HP * 4);       // [NSI][64]
     const sgmm_env_params p = params[ep.param[e]];
-    const float* g = gsm;
-    float w2f[NT][KS];
-    f32x4 b2c[NT];
-    float w1s[KS];
-#pragma unroll
-    for (int rt = 0; rt < NT; ++rt) {
-#pragma unroll
-        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + (16 * rt + col) * H + 4 * i + grp];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * grp + r];
-    }
-#pragma unroll
-    for (int i = 0; i < KS; ++i) w1s[i] = l1w[4 * i + grp][3];
-    const float b30 = g[L::B3], b31 = g[L::B3 + 1];
 
     // per-lane path bookkeeping: byte s of cur = the state of the path that
     // started the chunk in state s (tracked starts: bits of sset)
@@ -899,26 +903,35 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
     for (int s = 0; s < NSI; ++s) cnt[s] = 0;
     bool merged = __builtin_popcount(sset) <= 1;
     int kc = merged ? 0 : CL;
-    // the next tick's inputs, loaded one tick ahead
     auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
+#ifdef SGMM_STAMPS
+    // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
+    // slots and tile-slots run (slots 2, 3); nothing inside the loop waits
+    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
+#endif
+#ifdef SGMM_STAMPS_PHASE
+    // per wave (episode): 0 cycles, 1 tile-slots, 2 slots, 3 layer 1-3 cycles,
+    // 4 FPT-step cycles, 5 per-tick head (frontier, signals, layer-1 terms), 6 planes
+    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0};
+#define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+    SGMM_FT(fs_t0);
+#endif
     int64_t ti = tick_of(0);
-    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];
-    double nmid = tk.mid_next[ti], nask = tk.best_ask[ti], nbid = tk.best_bid[ti];
-    double nbmax = tk.buy_max[ti], nsmin = tk.sell_min[ti];
-    f32x4 acc[4][NT];
+    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
 #pragma unroll 1
     for (int tt = 0; tt < CL; ++tt) {
+#ifdef SGMM_STAMPS_PHASE
+        SGMM_FT(fs_a);
+#endif
         const bool act = tt < ntl;
         const float s1 = ns1, s2 = ns2;
-        const double tmid = nmid, task = nask, tbid = nbid, tbmax = nbmax, tsmin = nsmin;
+        // this tick's prices: first used after the tick's MLP, which hides the load
+        const double tmid = tk.mid_next[ti], task = tk.best_ask[ti], tbid = tk.best_bid[ti];
+        const double tbmax = tk.buy_max[ti], tsmin = tk.sell_min[ti];
         ti = tick_of(tt + 1);
         ns1 = tk.s1n[ti];
         ns2 = tk.s2n[ti];
-        nmid = tk.mid_next[ti];
-        nask = tk.best_ask[ti];
-        nbid = tk.best_bid[ti];
-        nbmax = tk.buy_max[ti];
-        nsmin = tk.sell_min[ti];
         // frontier: the distinct current states of the tracked paths
         uint32_t fmask = 0;
 #pragma unroll
@@ -935,10 +948,14 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
 #pragma unroll
         for (int q = 0; q < 4; ++q) tsl[q] = __builtin_amdgcn_readlane(ns, 16 * q);
         const int nslot = max(max(tsl[0], tsl[1]), max(tsl[2], tsl[3]));
-        // the weights stay in LDS (an opaque offset per tick keeps the compiler
-        // from hoisting them into ~90 registers across the tick loop)
-        int lofs = 0;
-        asm volatile("" : "+s"(lofs));
+#ifdef SGMM_STAMPS
+        lite_sl += nslot;
+        lite_ts += tsl[0] + tsl[1] + tsl[2] + tsl[3];
+#endif
+        // the weights stay in LDS: an opaque base per tick keeps the compiler
+        // from hoisting ~90 loop-invariant weight loads into registers
+        lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
+        asm volatile("" : "+v"(l1p));
         // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
         float pre[4][KS];
         {
@@ -950,34 +967,65 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
             }
 #pragma unroll
             for (int i = 0; i < KS; ++i) {
-                const f32x4 w = *reinterpret_cast<const f32x4*>(&l1w[4 * i + grp][0] + lofs);
+                const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
 #pragma unroll
                 for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
             }
         }
+#ifdef SGMM_STAMPS_PHASE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        SGMM_FT(fs_b);
+        fs_c[5] += fs_b - fs_a;
+        fs_c[2] += nslot;
+        fs_c[1] += (unsigned long long)(tsl[0] + tsl[1] + tsl[2] + tsl[3]);
+#endif
         uint32_t rem = fmask;
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
         uint32_t trm = 0;                 // bit f: a fill from frontier state f
 #pragma unroll 1
         for (int k = 0; k < nslot; ++k) {
-            int sofs = 0;
-            asm volatile("" : "+s"(sofs));
+            lds_cf* w3p = (lds_cf*)(&w3i[0]);
+            asm volatile("" : "+v"(w3p));
+            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
+            asm volatile("" : "+v"(w1p));
+            lds_cf* b2p = (lds_cf*)(&b2s[0]);
+            asm volatile("" : "+v"(b2p));
             const bool has = rem != 0u;
             const uint32_t f = has ? (uint32_t)__builtin_ctz(rem) : 0u;
             rem &= rem - 1u;
             const float x2own = (float)((double)(inv_min + (int)f) / 2.0);
+            // layer 1 + layer 2 for all four 16-lane tiles and both 16-neuron
+            // halves: 4 x NT independent accumulator chains issued k-step by
+            // k-step keep the matrix pipe busy (a tile-by-tile schedule waits
+            // ~40 cycles on every dependent MFMA); tiles without a k-th state
+            // compute and discard (they are the exception: 5.2 of 5.4 tile-slots run)
+            f32x4 acc[4][NT];
+            {
+                float x2q[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (k >= tsl[q]) continue;  // wave-uniform: no lane of tile q has a k-th state
-                const float x2 = __shfl(x2own, 16 * q + col, kWave);
+                for (int q = 0; q < 4; ++q) x2q[q] = __shfl(x2own, 16 * q + col, kWave);
 #pragma unroll
-                for (int i = 0; i < KS; ++i) {
-                    const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
+                for (int rt = 0; rt < NT; ++rt) {
+                    const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
 #pragma unroll
-                    for (int rt = 0; rt < NT; ++rt)
-                        acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1, i == 0 ? b2c[rt] : acc[q][rt],
-                                                                          0, 0, 0);
+                    for (int q = 0; q < 4; ++q) acc[q][rt] = bb;
                 }
+#pragma unroll
+                for (int i4 = 0; i4 < KS; i4 += 4) {
+                    const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pre[q][i4 + r]));
+#pragma unroll
+                            for (int rt = 0; rt < NT; ++rt)
+                                acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
+                        }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int rt = 0; rt < NT; ++rt) {
                     f32x4 v;
@@ -985,20 +1033,33 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
                     for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
                     *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
                 }
-            }
-            float o0 = b30, o1 = b31;
+            // layer 3 of this lane's sample, in neuron order (the canonical chain)
+            float o0 = w3p[2 * H], o1 = w3p[2 * H + 1];
+#pragma unroll 1
+            for (int j8 = 0; j8 < H / 8; ++j8) {
 #pragma unroll
-            for (int j4 = 0; j4 < H / 4; ++j4) {
-                const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j4 = 2 * j8 + jj;
+                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
 #pragma unroll
-                for (int r2 = 0; r2 < 2; ++r2) {
-                    const f32x4 w = *reinterpret_cast<const f32x4*>(&w3i[2 * (4 * j4 + 2 * r2)] + sofs);
-                    o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
-                    o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
-                    o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
-                    o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                    for (int r2 = 0; r2 < 2; ++r2) {
+                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
+                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                    }
                 }
             }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[3] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
             const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
             const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
             const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
@@ -1006,9 +1067,21 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
                 const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
                 stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
                 trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
-                rl[f][lane] = so1.reward;
+                rl[f * kWave + lane] = so1.reward;
             }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[4] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
         }
+#ifdef SGMM_STAMPS_PHASE
+        SGMM_FT(fs_b);
+#endif
         // the tick's rewards along the tracked paths; once they have merged only plane p0
         if (act) {
             const int64_t row = so + t0 + tt;
@@ -1016,7 +1089,7 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
             for (int s = 0; s < NSI; ++s) {
                 if (!((sset >> s) & 1u)) continue;
                 const uint32_t st = map_get(cur, (uint32_t)s);
-                if (!merged || (uint32_t)s == p0) rew[s * ep.rs + row] = rl[st][lane];
+                if (!merged || (uint32_t)s == p0) rew[s * ep.rs + row] = rl[st * kWave + lane];
                 cnt[s] += (trm >> st) & 1u;
             }
             cur = map_then(cur, stepmap);
@@ -1031,7 +1104,41 @@ __global__ __launch_bounds__(kWave) void k_policy_frontier(
                 }
             }
         }
+#ifdef SGMM_STAMPS_PHASE
+        {
+            unsigned long long t_;
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            SGMM_FT(t_);
+            fs_c[6] += t_ - fs_b;
+        }
+#endif
     }
+#ifdef SGMM_STAMPS_PHASE
+    {
+        unsigned long long t_;
+        SGMM_FT(t_);
+        fs_c[0] = t_ - fs_t0;
+        if (lane == 0 && e < kStampWaves)
+            for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
+    }
+#undef SGMM_FT
+#endif
+#ifdef SGMM_STAMPS
+    {
+        unsigned long long t1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        unsigned h_, x_;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(h_), "=s"(x_));
+        if (lane == 0 && e < kStampWaves) {
+            g_tstamps[e][0] = lite_t0;
+            g_tstamps[e][1] = t1;
+            g_tstamps[e][2] = lite_sl;
+            g_tstamps[e][3] = lite_ts;
+            g_thwid[e][0] = h_;
+            g_thwid[e][1] = x_;
+        }
+    }
+#endif
     if (lane < nch) {
         // untracked start states keep the identity byte (never on the episode's path)
         uint64_t cm = kIdentityMap;

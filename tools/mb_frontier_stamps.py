@@ -1,0 +1,51 @@
+"""Diagnostic: per-wave phase cycles of the frontier kernel (stamped library,
+tools/build_stamps.sh), on a config-3-shaped batch: P individuals x (one
+4560-tick training episode + one 912-tick validation episode), H=32.
+Per wave: 0 cycles, 1 tile-slots (16-lane MFMA tiles run), 2 slots (frontier
+passes), 3 layer 1-3 cycles, 4 FPT-step cycles, 5 per-tick head, 6 planes."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parent.parent
+os.environ["SGMM_LIB"] = str(ROOT / "tools/mb/libsgmm_stamps.so")
+os.environ["SGMM_TABLE_PATH"] = "frontier"
+sys.path.insert(0, str(ROOT))
+import numpy as np
+import torch
+import sgmm_pkg
+sg = sgmm_pkg.load()
+from sgmm_amd import _lib, synthetic
+L = _lib.load()
+L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+H = int(os.environ.get("H", 32))
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+sigma = float(sys.argv[2]) if len(sys.argv) > 2 else 0.05
+dev = torch.device("cuda")
+tr = synthetic.bundle_510300(4560, seed=0)
+va = synthetic.bundle_510300(912, seed=1)
+st = synthetic.train_stats(tr)
+ticks = sg.TickStore(); s0 = ticks.add(tr, st); s1 = ticks.add(va, st); ticks.to(dev)
+params = sg.params_tensor([sg.EnvConfig(phi=1e-3, tick_size=0.001)], dev)
+pop = synthetic.population(P, H, sigma=sigma, seed=1).to(dev)
+offs = [ticks.segments[s0][0]] * P + [ticks.segments[s1][0]] * P
+lens = [4560] * P + [912] * P
+eb = sg.EpisodeBatch(np.r_[np.arange(P), np.arange(P)], offs, lens, np.zeros(2 * P)).to(dev)
+eng = sg.RolloutEngine(dev)
+for _ in range(3):
+    eng.fitness(ticks, eb, params, pop, H)
+torch.cuda.synchronize()
+n = 2 * P
+h = np.zeros((n, 8), np.uint64)
+L.sgmm_debug_tstamps(h.ctypes.data, n)
+h = h.astype(np.float64)
+for name, sl, T in (("train", slice(0, P), 4560), ("val", slice(P, 2 * P), 912)):
+    x = h[sl]
+    CL = max(4, ((T + 63) // 64 + 3) // 4 * 4)
+    med = lambda a: float(np.median(a))
+    print(f"{name}: T={T} chunk={CL} waves={len(x)}")
+    print(f"  cycles/wave {med(x[:, 0]):9.0f}   per tick {med(x[:, 0]) / CL:7.0f}")
+    print(f"  slots/tick {med(x[:, 2]) / CL:5.2f}   tile-slots/tick {med(x[:, 1]) / CL:5.2f}")
+    for k, lab in ((3, "layer 1-3"), (4, "FPT step"), (5, "tick head"), (6, "planes")):
+        print(f"  {lab:10s} {med(x[:, k]):9.0f} cyc/wave = {med(x[:, k]) / med(x[:, 0]) * 100:5.1f} %"
+              f"   per slot {med(x[:, k]) / max(1, med(x[:, 2])):6.0f}   per tile-slot {med(x[:, k]) / max(1, med(x[:, 1])):6.0f}")

@@ -1,0 +1,67 @@
+"""Diagnostic: wave timeline of the frontier kernel (stamped library): per wave
+(episode) its start / end (s_memrealtime, 100 MHz), SIMD / CU / XCD, slots.
+Config-3 shape: 5 x P individuals x (4560-tick training + 912-tick validation
+episode), H=32, episodes in the GA session's order."""
+import ctypes
+import os
+import sys
+from pathlib import Path
+ROOT = Path(__file__).resolve().parent.parent
+os.environ["SGMM_LIB"] = str(ROOT / "tools/mb/libsgmm_stamps.so")
+os.environ["SGMM_TABLE_PATH"] = "frontier"
+sys.path.insert(0, str(ROOT))
+import numpy as np
+import torch
+import sgmm_pkg
+sg = sgmm_pkg.load()
+from sgmm_amd import _lib, synthetic
+L = _lib.load()
+L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_thwid.argtypes = [ctypes.c_void_p, ctypes.c_int]
+H, K = 32, 5
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 512
+dev = torch.device("cuda")
+tr = synthetic.bundle_510300(4560, seed=0)
+va = synthetic.bundle_510300(912, seed=1)
+st = synthetic.train_stats(tr)
+ticks = sg.TickStore(); s0 = ticks.add(tr, st); s1 = ticks.add(va, st); ticks.to(dev)
+params = sg.params_tensor([sg.EnvConfig(phi=1e-3, tick_size=0.001)], dev)
+pop = synthetic.population(K * P, H, sigma=0.05, seed=1).to(dev)
+gen, offs, lens = [], [], []
+for k in range(K):
+    gen += list(range(k * P, (k + 1) * P)) * 2
+    offs += [ticks.segments[s0][0]] * P + [ticks.segments[s1][0]] * P
+    lens += [4560] * P + [912] * P
+n = len(gen)
+eb = sg.EpisodeBatch(np.array(gen), offs, lens, np.zeros(n)).to(dev)
+eng = sg.RolloutEngine(dev)
+for _ in range(3):
+    eng.fitness(ticks, eb, params, pop, H)
+torch.cuda.synchronize()
+h = np.zeros((n, 8), np.uint64)
+L.sgmm_debug_tstamps(h.ctypes.data, n)
+hw = np.zeros((n, 2), np.uint32)
+L.sgmm_debug_thwid(hw.ctypes.data, n)
+t0 = h[:, 0].astype(np.int64); t1 = h[:, 1].astype(np.int64)
+base = t0.min()
+s, e_ = (t0 - base) * 10, (t1 - base) * 10  # ns
+dur = e_ - s
+simd = (hw[:, 0] >> 4) & 3; cu = (hw[:, 0] >> 8) & 15; se = (hw[:, 0] >> 13) & 7; xcc = hw[:, 1] & 7
+sid = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+lens = np.array(lens)
+print(f"waves {n}; kernel span {e_.max() / 1e3:.1f} us; distinct SIMDs {len(np.unique(sid))}")
+for name, m in (("train", lens == 4560), ("val", lens == 912)):
+    print(f"  {name}: duration med {np.median(dur[m]) / 1e3:.1f} us p10 {np.percentile(dur[m], 10) / 1e3:.1f} "
+          f"p90 {np.percentile(dur[m], 90) / 1e3:.1f}; start med {np.median(s[m]) / 1e3:.1f} us "
+          f"max {s[m].max() / 1e3:.1f}; slots/wave {np.median(h[m, 2]):.0f} tile-slots {np.median(h[m, 3]):.0f}")
+# per-SIMD busy: sum of wave durations and concurrency
+u, inv = np.unique(sid, return_inverse=True)
+busy = np.bincount(inv, weights=dur)
+cnt = np.bincount(inv)
+last = np.zeros(len(u)); np.maximum.at(last, inv, e_)
+print(f"  waves per SIMD: mean {cnt.mean():.2f} max {cnt.max()}; per-SIMD sum of wave time / span: "
+      f"med {np.median(busy / last):.2f}; SIMD last end: med {np.median(last) / 1e3:.1f} us max {last.max() / 1e3:.1f}")
+# concurrency histogram over time
+grid = np.linspace(0, e_.max(), 40)
+act = [(np.sum((s <= t) & (e_ > t))) for t in grid]
+print("  resident waves over time (/1024 SIMDs):", [round(a / 1024, 2) for a in act[::4]])
