@@ -285,24 +285,29 @@ def main():
     kernels = {k: {"avg_us": 1e3 * v[0] / v[1], "launches": v[1]} for k, v in prof.items()}
     gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, args.profile_steps)
 
-    # roofline of the policy-table kernel (the FP32 compute kernel of the path)
+    # roofline of the policy kernel (the FP32 compute kernel of the path): the
+    # frontier kernel from 2048 episodes per launch, the table below that
     steps_per_launch = K * n_rank * (T + Tv)  # fused validation: train + validation episodes
     fl = flop_per_step(H)
-    tab = kernels.get("policy_table")
+    kname = "policy_frontier" if "policy_frontier" in kernels else "policy_table"
+    tab = kernels.get(kname)
     pmc = latest_pmc(args.pmc, args.config)
     roofline = None
     if tab:
         achieved = steps_per_launch * fl / (tab["avg_us"] * 1e-6) / 1e12
         traffic = None
-        if pmc and pmc.get("kernels", {}).get("policy_table"):
-            traffic = pmc["kernels"]["policy_table"].get("hbm_bytes_per_launch")
+        if pmc and pmc.get("kernels", {}).get(kname):
+            traffic = pmc["kernels"][kname].get("hbm_bytes_per_launch")
+        note = ("algorithmic = one policy forward per env-step (train + validation ticks of one launch). "
+                + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.35 per "
+                   "training tick on this workload, in 16-lane MFMA tiles)" if kname == "policy_frontier" else
+                   "k_policy_table_v3 evaluates every inventory state (5x this work)"))
         roofline = {"bound": "mfma", "pipe": "fp32 (gfx950 f32 MFMA peak == f32 VALU peak)",
-                    "kernel": "k_policy_table_mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
+                    "kernel": "k_policy_frontier" if kname == "policy_frontier" else "k_policy_table_v3",
+                    "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                     "algorithmic": {"flop_per_env_step": fl, "env_steps_per_launch": steps_per_launch,
-                                    "note": "algorithmic = one policy forward per env-step (train + validation "
-                                            "ticks of one launch); the table kernel evaluates every inventory "
-                                            "state (5x this work)"},
+                                    "note": note},
                     "avg_launch_us": tab["avg_us"]}
         if traffic:
             gbps = traffic / (tab["avg_us"] * 1e-6) / 1e9

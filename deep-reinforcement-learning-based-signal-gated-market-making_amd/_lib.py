@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading libsgmm.so, see module doc)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("SGMM_LIB", PKG_DIR / "libsgmm.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class SgmmError(RuntimeError):
@@ -43,7 +43,7 @@ class Episodes(ctypes.Structure):
                 ("inv_max", ctypes.c_int32), ("genome", ctypes.c_void_p),
                 ("adv", ctypes.c_void_p), ("tick_off", ctypes.c_void_p),
                 ("len", ctypes.c_void_p), ("step_off", ctypes.c_void_p),
-                ("param", ctypes.c_void_p)]
+                ("param", ctypes.c_void_p), ("order", ctypes.c_void_p)]
 
 
 class GAState(ctypes.Structure):

@@ -52,6 +52,7 @@ struct EpArrays {
     const int64_t* step_off;
     const int32_t* param;
     int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
+    const int32_t* order;  // frontier kernel: episode of workgroup b (NULL: b)
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16, KS = H / 4;
     constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
-    const int e = blockIdx.x;
+    const int e = ep.order ? ep.order[blockIdx.x] : (int)blockIdx.x;  // longest episodes first
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
     const int CL = frontier_len(T);
@@ -1936,7 +1937,7 @@ static int64_t rew_stride(int64_t steps) { return (steps + 31) & ~int64_t(31); }
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps)};
+                    e->param, rew_stride(e->total_steps), e->order};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -2133,7 +2134,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
     if (fr && eps->max_len > 0) {
-        ProfScope prof("policy_table", s);
+        ProfScope prof("policy_frontier", s);
         const dim3 grid(eps->n), block(kWave);
 #define SGMM_FRONTIER(H_, NSI_)                                                                            \
     SGMM_LAUNCH((k_policy_frontier<H_, NSI_>), grid, block, 0, s, *ticks, ep, params, src, eps->inv_min, nsi, \

@@ -120,13 +120,15 @@ class EpisodeBatch:
             if len(self.length) else np.zeros(0, np.int64)
         self.total_steps = int(self.length.astype(np.int64).sum())
         self.max_len = int(self.length.max()) if len(self.length) else 0
+        # longest first (stable): the frontier kernel's processing order
+        self.order = np.argsort(-self.length.astype(np.int64), kind="stable").astype(np.int32)
 
     @property
     def n(self):
         return len(self.genome)
 
     def to(self, device):
-        for k in ("genome", "tick_off", "length", "param", "step_off", "adv"):
+        for k in ("genome", "tick_off", "length", "param", "step_off", "adv", "order"):
             v = getattr(self, k)
             self.dev[k] = None if v is None else torch.from_numpy(v).to(device)
         return self
@@ -136,7 +138,7 @@ class EpisodeBatch:
         return Episodes(self.n, self.max_len, self.total_steps, self.inv_min, self.inv_max,
                         d["genome"].data_ptr(), d["adv"].data_ptr() if d["adv"] is not None else None,
                         d["tick_off"].data_ptr(), d["length"].data_ptr(), d["step_off"].data_ptr(),
-                        d["param"].data_ptr())
+                        d["param"].data_ptr(), d["order"].data_ptr() if d.get("order") is not None else None)
 
 
 class RolloutEngine:

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SGMM_ABI_VERSION 1
+#define SGMM_ABI_VERSION 2
 
 enum {
     SGMM_OK = 0,
@@ -75,7 +75,10 @@ typedef struct sgmm_ticks {
  * with params[param[e]].  step_off = exclusive prefix sum of len (it places
  * each episode's tables in the workspace); total_steps = sum of len.
  * Every episode of one call shares the inventory range [inv_min, inv_max]
- * (at most 8 inventory values; 0 must lie inside). */
+ * (at most 8 inventory values; 0 must lie inside).  order (optional, may be
+ * NULL) is a permutation of [0, n), longest episode first: the frontier
+ * kernel (one wave per episode) starts the longest walks first so short ones
+ * fill the tail; results are per episode and do not depend on it. */
 typedef struct sgmm_episodes {
     int32_t        n;
     int32_t        max_len;
@@ -88,6 +91,7 @@ typedef struct sgmm_episodes {
     const int32_t *len;
     const int64_t *step_off;
     const int32_t *param;
+    const int32_t *order;     /* may be NULL: identity (ABI 2) */
 } sgmm_episodes;
 
 int         sgmm_abi_version(void);

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(sgmm):
     assert declared <= exported, declared - exported
     assert exported <= declared, exported - declared  # nothing undocumented
     assert set(_lib.SIGNATURES) == declared            # the binding covers the header
-    assert L.sgmm_abi_version() == 1
+    assert L.sgmm_abi_version() == 2
 
 
 def test_struct_layouts_match_header(sgmm):
@@ -42,7 +42,7 @@ def test_struct_layouts_match_header(sgmm):
     assert ctypes.sizeof(_lib.EnvParams) == 48
     assert ctypes.sizeof(_lib.GAState) == 80 and _lib.GAState.decay.offset == 72
     assert ctypes.sizeof(_lib.GAHistory) == 40
-    assert _lib.Episodes.genome.offset == 24 and ctypes.sizeof(_lib.Episodes) == 72
+    assert _lib.Episodes.genome.offset == 24 and ctypes.sizeof(_lib.Episodes) == 80
     assert ctypes.sizeof(_lib.Ticks) == 56
     assert ctypes.sizeof(_lib.AskedPopulation) == 40 and _lib.AskedPopulation.i0.offset == 32
     assert _lib.GAState.arrivals.offset == 68

@@ -13,7 +13,7 @@ import glob
 import json
 import sys
 
-KINDS = ("policy_table", "path_scan", "ga_step", "rollout_direct", "ordered_sum")
+KINDS = ("policy_table", "policy_frontier", "path_scan", "ga_step", "rollout_direct", "ordered_sum")
 
 
 def kind(name):

@@ -12,7 +12,7 @@ import glob
 import json
 import sys
 
-KIND = (("policy_table", "policy_table"), ("path_scan", "path_scan"), ("ga_step", "ga_step"),
+KIND = (("policy_table", "policy_table"), ("policy_frontier", "policy_frontier"), ("path_scan", "path_scan"), ("ga_step", "ga_step"),
         ("ga_ask", "ga_ask"), ("ga_tell", "ga_tell"), ("ga_val_update", "ga_val_update"))
 
 
