@@ -1559,14 +1559,18 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
 //   2. every thread: the rewards of its 4 ticks from the path plane of their
 //      chunk's start state (one coalesced row per chunk) -> LDS;
 //   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
-template <int NSM, int NT, bool FR>
-__global__ __launch_bounds__(NT) void k_path_scan(
+template <int NSM, int NT, bool FR, int TPB = NT>
+__global__ __launch_bounds__(TPB) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
     const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
     const uint32_t* __restrict__ kinfo, const double* __restrict__ rew, double* __restrict__ fitness,
     int32_t* __restrict__ trades_out, StepArgs step) {
     // FR: the frontier kernel's chunks (frontier_len(T) ticks, at most 64 per
-    // episode, slots e * 64 + c, u32 trade counts, kinfo = merge tick | p0 << 29)
+    // episode, slots e * 64 + c, u32 trade counts, kinfo = merge tick | p0 << 29).
+    // TPB < NT: a TPB-thread workgroup with NT's window and block layout
+    // (TPB = 64, NT = 256: one wave -- the only one exact_sum_window<256> gives
+    // blocks to -- gathers 1024 values, so many more episodes run per CU)
+    static_assert(TPB == NT || (TPB == kWave && NT == 4 * kWave), "TPB = NT or one wave with NT = 256");
     constexpr int kWin = NT * kSumTpt;
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);  // [kWin]
@@ -1613,7 +1617,9 @@ __global__ __launch_bounds__(NT) void k_path_scan(
     double S = 0.0;  // exact running sum (identical in every thread between windows)
     for (int w0 = 0; w0 < T; w0 += kWin) {
         const int n = min(kWin, T - w0);
-        const int i0 = tid * kSumTpt;
+#pragma unroll
+        for (int g = 0; g < NT / TPB; ++g) {
+        const int i0 = (g * TPB + tid) * kSumTpt;
         if (i0 < n) {  // 4 ticks of one chunk (CL % kSumTpt == 0)
             double r[kSumTpt];
             if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
@@ -1634,6 +1640,7 @@ __global__ __launch_bounds__(NT) void k_path_scan(
 #pragma unroll
             for (int j = 0; j < kSumTpt; ++j)
                 if (i0 + j < n) sel[i0 + j] = r[j];
+        }
         }
         __syncthreads();
         SGMM_STAMP(e, 2);
@@ -2080,7 +2087,14 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
 // path-scan workgroup size for n episodes (256 CUs): one 16-wave workgroup per
 // CU while they fit, then 8-wave, then 4-wave workgroups
 static int scan_threads(int64_t n) {
-    return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : 256);
+    if (const char* v = std::getenv("SGMM_SCAN_THREADS")) {
+        const int t = std::atoi(v);
+        if (t == 64 || t == 256 || t == 512 || t == 1024) return t;
+    }
+    // beyond 1024 episodes one-wave workgroups: the exact-sum walk is serial,
+    // so ~15 episodes resident per CU beat 4 wider workgroups (config 3:
+    // 193 -> 145 us per scan, tools/gpu_sc1.sh)
+    return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : kWave);
 }
 
 template <int NSM, bool FR>
@@ -2088,7 +2102,10 @@ static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const
                              const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
                              const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
                              int32_t* trades, const StepArgs& step) {
-    if (nt == kScanThreads)
+    if (nt == kWave)
+        SGMM_LAUNCH((k_path_scan<NSM, 4 * kWave, FR, kWave>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, kinfo, rew, fitness, trades, step);
+    else if (nt == kScanThreads)
         SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
                     cmaps, ctr, kinfo, rew, fitness, trades, step);
     else if (nt == 512)
@@ -2183,7 +2200,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         // resident per CU, so the serial walks of different episodes overlap
         // instead of idling the CU (A/B on MI355X: P=64 / 256 / 1024 / 4096)
         const int nt = scan_threads(eps->n);
-        size_t lds = (size_t)nt * kSumTpt * sizeof(double);
+        size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double);  // the window
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
         if (fr) {
             if (nsi <= 5)
