@@ -841,6 +841,12 @@ __host__ __device__ __forceinline__ int frontier_len(int T) {
     const int c = (T + kFrontierSlots - 1) / kFrontierSlots;
     return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
 }
+// the episode's block of plane rows: frontier_len(T) x 64 <= T + 256 slots
+// (T rounded up to 64 chunks of a multiple of 4), so blocks at step_off + 256 e
+// never overlap; the plane stride covers total_steps + 256 n (rew_stride)
+__device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
+    return step_off + (int64_t)4 * kFrontierSlots * e;
+}
 
 template <int H, int NSI>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(
@@ -1085,7 +1091,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #endif
         // the tick's rewards along the tracked paths; once they have merged only plane p0
         if (act) {
-            const int64_t row = so + t0 + tt;
+            // planes in tick-offset-major order (row u of an episode's block holds
+            // the 64 chunks' rewards at offset u): one coalesced 512-byte store
+            // per plane and tick; row-major rows made every 8-byte store a
+            // partial line and the L2 wrote ~6x the bytes back
+            const int64_t row = frontier_base(so, e) + (int64_t)tt * kFrontierSlots + lane;
 #pragma unroll
             for (int s = 0; s < NSI; ++s) {
                 if (!((sset >> s) & 1u)) continue;
@@ -1627,10 +1637,11 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
                 const uint32_t ki = kin[c];
                 const int kc = (int)(ki & 0x1FFFFFFFu);
                 const int64_t pst = start[c], pp0 = ki >> 29;
+                const int64_t rb = frontier_base(so, e) + c;
 #pragma unroll
                 for (int j = 0; j < kSumTpt; ++j) {
                     const int jj = min(j, n - 1 - i0);
-                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + so + w0 + i0 + jj];
+                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierSlots];
                 }
             } else {
                 const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
@@ -1940,11 +1951,12 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     return SGMM_OK;
 }
 
-static int64_t rew_stride(int64_t steps) { return (steps + 31) & ~int64_t(31); }
+// plane stride: every tick plus the frontier layout's 256 padding slots per episode
+static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + 256 * n + 31) & ~int64_t(31); }
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps), e->order};
+                    e->param, rew_stride(e->total_steps, e->n), e->order};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -2003,7 +2015,7 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
     if (n_states > 8)  // adversary: rew[row * n_states + state]
         return ws_fills(total_steps) + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           (size_t)rew_stride(total_steps) * (size_t)n_states * sizeof(double);
+           (size_t)rew_stride(total_steps, n_episodes) * (size_t)n_states * sizeof(double);
 }
 
 // Frontier kernel or table: the frontier kernel does ~1/3 of the table's

@@ -61,7 +61,8 @@ def test_argument_errors_need_no_gpu(sgmm):
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
     # frontier kernel (64 chunk slots per episode: u64 map, u32[8] counts, u32 merge info)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == 4 * 64 * 8 + 4 * 64 * 32 + 4 * 64 * 4 + 5 * 1024 * 8
+    # (planes: 1000 ticks + 256 padding slots per episode of the frontier layout, rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == 4 * 64 * 8 + 4 * 64 * 32 + 4 * 64 * 4 + 5 * 2048 * 8
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)
