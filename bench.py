@@ -327,7 +327,9 @@ def main():
                        "phis": [p for p, _, _ in spec["pops"]], "hidden": H, "ticks_train": T, "ticks_val": Tv,
                        "adversary": spec["arl"], "val_mode": "fused",
                        "parallelism": f"population shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
-                       "hip_graph": bool(sess.use_graph)},
+                       "hip_graph": bool(sess.use_graph),
+                       "graph_has_exchange": bool(sess.full_graph) if world > 1 else None,
+                       "graph_capture_error": getattr(sess, "capture_error", None)},
             "generations_per_s": gens_per_s,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -149,14 +149,17 @@ class DRLEngine:
       dist        -- torch.distributed group (None = default if initialised,
                      False = single process): the population is sharded over ranks
                      and fitness is all-gathered once per generation.
-      use_graph   -- capture one generation in a HIP graph and replay it
-                     (single process, rng="device").
+      use_graph   -- capture generations in HIP graphs and replay them (rng="device");
+                     with several ranks on RCCL the all-gather is captured too.
+      exchange    -- "auto": shard + all-gather only with several ranks; "always":
+                     take the sharded path (asked rollout, all-gather, GA step) on
+                     one process too -- the multi-GPU path rehearsed on one GPU.
     """
 
     def __init__(self, pop_size=50, sigma=0.05, phi=0.01, tick_size=0.01, fee_rate=0.0,
                  use_arl=False, save_dir="checkpoints/drl", *, hidden_dim=32, rng="device",
                  seed=None, val_mode="auto", honor_sigma=False, sync_every=10, dist=None,
-                 device=None, verbose=True, patience=15, decay=0.5, use_graph=True):
+                 device=None, verbose=True, patience=15, decay=0.5, use_graph=True, exchange="auto"):
         self.phi = phi
         self.tick_size = tick_size
         self.fee_rate = fee_rate
@@ -187,6 +190,9 @@ class DRLEngine:
         self.patience = int(patience)
         self.decay = float(decay)
         self.use_graph = use_graph
+        if exchange not in ("auto", "always"):
+            raise ValueError("exchange must be 'auto' or 'always'")
+        self.exchange = exchange
         self.timing = {}
 
     def _log(self, msg):
@@ -208,7 +214,97 @@ class DRLEngine:
         return sess.finish()
 
 
-class TrainingSession:
+class _GraphedGenerations:
+    """Generation replay shared by TrainingSession and MultiSession.
+
+    A generation is _rollout, _exchange, _boundary (the last two no-ops on one
+    unsharded process).  With use_graph it is captured once and replayed; when
+    the exchange is capturable -- one process, or RCCL (nccl backend) -- the
+    whole generation, all-gather included, is ONE graph, and batches of
+    GRAPH_BATCH generations are captured into one graph as well, so several
+    ranks also run one host launch per batch.  Otherwise (gloo: the gather is
+    staged through host memory) the rollout and the GA step are two graphs
+    around an eager all-gather."""
+
+    # generations per captured multi-generation graph
+    GRAPH_BATCH = 16
+
+    def _gen(self):
+        self._rollout()
+        self._exchange()
+        self._boundary()
+
+    def _collective_capturable(self) -> bool:
+        if not self.sharded:
+            return True
+        import torch.distributed as tdist
+        if not (tdist.is_available() and tdist.is_initialized()):
+            return True  # one process without a group: the gather is a device copy
+        return tdist.get_backend(self.group) == "nccl"
+
+    def capture(self):
+        """Record (without running) the generation graph(s) and the batch graph."""
+        if not self.use_graph:
+            return
+        if self.graphs is None:
+            if self._collective_capturable():
+                try:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        self._gen()
+                    self.graphs, self.full_graph = [g], True
+                except Exception as ex:  # an RCCL build that cannot capture: eager exchange
+                    if not self.sharded:
+                        raise
+                    self.full_graph = False
+                    self.capture_error = repr(ex)
+            if not self.full_graph:
+                self.graphs = []
+                for fn in (self._rollout, self._boundary):
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g):
+                        fn()
+                    self.graphs.append(g)
+        if self.full_graph and self.graph_batch > 1 and self.batch_graph is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.graph_batch):
+                    self._gen()
+            self.batch_graph = g
+
+    def step(self, gen: int):
+        """Enqueue generation ``gen`` (drl_engine.py:92-171) on the current stream."""
+        if not self.use_graph:
+            self._gen()
+            return
+        self.capture()
+        if self.full_graph:
+            self.graphs[0].replay()
+        else:
+            self.graphs[0].replay()
+            self._exchange()
+            self.graphs[1].replay()
+
+    def steps(self, gen0: int, n: int):
+        """Enqueue generations gen0 .. gen0 + n - 1 (same as n step() calls):
+        whole batches replay the batch graph (one host launch per batch; the
+        host-side launch, not the GPU, paced single-generation replays)."""
+        if self.use_graph:
+            self.capture()
+        if not self.use_graph or not self.full_graph:
+            for g in range(gen0, gen0 + n):
+                self.step(g)
+            return
+        B, done = self.graph_batch, 0
+        if B > 1 and n >= B:
+            while n - done >= B:
+                self.batch_graph.replay()
+                done += B
+        for g in range(gen0 + done, gen0 + n):
+            self.step(g)
+
+
+class TrainingSession(_GraphedGenerations):
     """One DRLEngine.train run, resident on the GPU (drl_engine.py:83-178).
 
     Per generation (step): ask the shard's genomes -> roll the shard out (train,
@@ -225,6 +321,7 @@ class TrainingSession:
         dev = self.dev = self.roll.device
         self.L = self.roll.L
         self.group, self.rank, self.world = _dist_info(eng.dist)
+        self.sharded = self.world > 1 or eng.exchange == "always"
         P, H = eng.pop_size, eng.hidden_dim
         self.P, self.H, self.G = P, H, genome_size(H)
         G = self.G
@@ -251,7 +348,7 @@ class TrainingSession:
 
         g_tr, o_tr, l_tr = phase(tr_off, self.T_tr)
         g_va, o_va, l_va = phase(va_off, self.T_va)
-        self.rec = FitnessRecords(P, self.world, dev)
+        self.rec = FitnessRecords(P, self.world, dev, gather=self.sharded)
         if self.fused:  # one launch: training + validation episodes of the shard
             adv = np.concatenate([g_tr, np.full(n_cap, -1)]) if arl else None  # validation: no adversary
             self.train_eps = EpisodeBatch(np.concatenate([g_tr, g_va]), np.concatenate([o_tr, o_va]),
@@ -298,7 +395,7 @@ class TrainingSession:
         # generation on one rank; with several ranks the rollout and the boundary
         # are captured separately around the (eager) all-gather
         self.use_graph = bool(eng.use_graph) and not self.torch_rng
-        self.graphs = None
+        self.graphs, self.batch_graph, self.full_graph = None, None, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, eng.sync_every))
         self.roll.reserve(self.train_eps, arl)
         if self.val_eps is not None:
@@ -310,69 +407,6 @@ class TrainingSession:
         self.ev0 = torch.cuda.Event(enable_timing=True)
         self.ev1 = torch.cuda.Event(enable_timing=True)
         self.ev0.record()
-
-    def step(self, gen: int):
-        """Enqueue generation ``gen`` (drl_engine.py:92-171) on the current stream.
-
-        With use_graph the generation's launches (whose arguments never change:
-        gen and sigma live in the device GA state) are captured once in HIP
-        graphs and replayed."""
-        if not self.use_graph:
-            self._rollout()
-            self._exchange()
-            self._boundary()
-            return
-        self.capture()
-        self.graphs[0].replay()
-        if self.world > 1:
-            self._exchange()
-            self.graphs[1].replay()
-
-    # generations per captured multi-generation graph (one process)
-    GRAPH_BATCH = 16
-
-    def capture(self):
-        """Record (without running) the generation graphs: one generation, and
-        with one process a batch of min(GRAPH_BATCH, sync_every) generations."""
-        if not self.use_graph:
-            return
-        if self.graphs is None:
-            self.graphs = []
-            phases = [(self._rollout, self._boundary)] if self.world == 1 else [(self._rollout,), (self._boundary,)]
-            for fns in phases:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for f in fns:
-                        f()
-                self.graphs.append(g)
-        if self.world == 1 and self.graph_batch > 1 and getattr(self, "batch_graph", None) is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(self.graph_batch):
-                    self._rollout()
-                    self._boundary()
-            self.batch_graph = g
-
-    def steps(self, gen0: int, n: int):
-        """Enqueue generations gen0 .. gen0 + n - 1 (same as n step() calls).
-
-        With one process and use_graph, whole batches of GRAPH_BATCH
-        generations are captured once in a single HIP graph and replayed: one
-        host launch per batch instead of per generation (the host-side graph
-        launch, not the GPU, set the pace of single-generation replays)."""
-        if not self.use_graph or self.world > 1:
-            for g in range(gen0, gen0 + n):
-                self.step(g)
-            return
-        B = self.graph_batch
-        done = 0
-        if B > 1 and n >= B:
-            self.capture()
-            while n - done >= B:
-                self.batch_graph.replay()
-                done += B
-        for g in range(gen0 + done, gen0 + n):
-            self.step(g)
 
     def _ask(self):
         """ask() of the shard (models/model.py:65-71) from the device master/sigma."""
@@ -394,7 +428,7 @@ class TrainingSession:
             tk, ep = self.ticks.struct(), self.train_eps.struct()
             ws = self.roll.workspace(self.train_eps, self.arl)
             f, t = self.out
-            if self.world == 1:
+            if not self.sharded:
                 check(L.sgmm_generation(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params), ptr(self.state),
                                         ptr(self.master), ptr(self.master_adv) if self.arl else None,
                                         ptr(self.best_master), self.H, self.e.seed, P, ptr(f), ptr(t),
@@ -417,7 +451,7 @@ class TrainingSession:
 
     def _exchange(self):
         """The generation's one collective: all-gather the per-rank records."""
-        if self.world > 1:
+        if self.sharded:
             self.rec.all_gather(self.group)
 
     def _boundary(self):
@@ -427,7 +461,7 @@ class TrainingSession:
         P, G = self.P, self.G
         arl = self.arl
         if self.fast_step:
-            if self.world > 1:
+            if self.sharded:
                 check(L.sgmm_ga_step(ptr(self.state), *self.rec.step_args(),
                                      ptr(self.master), ptr(self.master_adv) if arl else None,
                                      ptr(self.best_master), G, ADV_GENOME if arl else 0, e.seed,
@@ -573,13 +607,11 @@ def _per_pop(x, K):
     return x
 
 
-class MultiSession:
+class MultiSession(_GraphedGenerations):
     """K DRLEngine.train runs resident on the GPU, one launch pair per
     generation for all of them (sgmm_generation_multi), or -- with several
     ranks -- the asked rollout of every population's shard, one all-gather of
     the K records and one K-workgroup GA step (sgmm_ga_step_multi)."""
-
-    GRAPH_BATCH = TrainingSession.GRAPH_BATCH
 
     def __init__(self, meng: MultiDRLEngine, train_bundles, val_bundles, train_stats, generations,
                  output_prefix):
@@ -592,6 +624,7 @@ class MultiSession:
         dev = self.dev = self.roll.device
         self.L = self.roll.L
         self.group, self.rank, self.world = _dist_info(e0.dist)
+        self.sharded = self.world > 1 or e0.exchange == "always"
         P, H = self.P, self.H = e0.pop_size, e0.hidden_dim
         G = self.G = genome_size(H)
         self.i0, self.i1 = shard_bounds(P, self.rank, self.world)
@@ -627,7 +660,7 @@ class MultiSession:
                 adv.append(g[-1] if is_tr else np.full(n, -1))  # validation: no adversary
         self.eps = EpisodeBatch(np.concatenate(g), np.concatenate(off), np.concatenate(ln), np.concatenate(par),
                                 adv=np.concatenate(adv) if arl else None).to(dev)
-        self.rec = FitnessRecords(P, self.world, dev, n_pop=K)
+        self.rec = FitnessRecords(P, self.world, dev, n_pop=K, gather=self.sharded)
         f32 = dict(dtype=torch.float32, device=dev)
         self.masters = torch.stack([e.mm_evolver.master_policy.get_weights() for e in engs]).to(**f32).contiguous()
         self.masters_adv = torch.stack([e.adv_evolver.master_policy.get_weights() for e in engs]).to(**f32) \
@@ -645,8 +678,7 @@ class MultiSession:
                                      self.masters_adv.data_ptr() if arl else None, self.best_masters.data_ptr(),
                                      self.seeds.data_ptr(), self.hist.data_ptr())
         self.use_graph = bool(e0.use_graph)
-        self.graphs = None
-        self.batch_graph = None
+        self.graphs, self.batch_graph, self.full_graph = None, None, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, e0.sync_every))
         self.roll.reserve(self.eps, arl)
         self.best_paths = [os.path.join(e.save_dir, f"{output_prefix}_best_val_{e.phi}.pth") for e in engs]
@@ -660,7 +692,7 @@ class MultiSession:
         tk, ep = self.ticks.struct(), self.eps.struct()
         ws = self.roll.workspace(self.eps, self.arl)
         f, t = self.rec.both
-        if self.world == 1:
+        if not self.sharded:
             check(self.L.sgmm_generation_multi(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
                                                ctypes.byref(self.pops), ptr(f), ptr(t), ptr(ws), ws.numel(),
                                                stream_ptr()), "sgmm_generation_multi")
@@ -671,58 +703,13 @@ class MultiSession:
                   "sgmm_rollout_fitness_asked_multi")
 
     def _exchange(self):
-        if self.world > 1:
+        if self.sharded:
             self.rec.all_gather(self.group)
 
     def _boundary(self):
-        if self.world > 1:
+        if self.sharded:
             check(self.L.sgmm_ga_step_multi(ctypes.byref(self.pops), *self.rec.multi_step_args(), stream_ptr()),
                   "sgmm_ga_step_multi")
-
-    def capture(self):
-        if not self.use_graph:
-            return
-        if self.graphs is None:
-            self.graphs = []
-            phases = [(self._rollout,)] if self.world == 1 else [(self._rollout,), (self._boundary,)]
-            for fns in phases:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for fn in fns:
-                        fn()
-                self.graphs.append(g)
-        if self.world == 1 and self.graph_batch > 1 and self.batch_graph is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(self.graph_batch):
-                    self._rollout()
-            self.batch_graph = g
-
-    def step(self, gen: int):
-        if not self.use_graph:
-            self._rollout()
-            self._exchange()
-            self._boundary()
-            return
-        self.capture()
-        self.graphs[0].replay()
-        if self.world > 1:
-            self._exchange()
-            self.graphs[1].replay()
-
-    def steps(self, gen0: int, n: int):
-        if not self.use_graph or self.world > 1:
-            for g in range(gen0, gen0 + n):
-                self.step(g)
-            return
-        B, done = self.graph_batch, 0
-        if B > 1 and n >= B:
-            self.capture()
-            while n - done >= B:
-                self.batch_graph.replay()
-                done += B
-        for g in range(gen0 + done, gen0 + n):
-            self.step(g)
 
     def flush(self, upto: int):
         """History rows [emitted, upto) of every population: the reference's log

@@ -58,8 +58,11 @@ class FitnessRecords:
     fields sit at k * 16n (fitness) and 16Kn + k * 8n (trades) -- K = 1 is the
     single-population layout above."""
 
-    def __init__(self, P: int, world: int, device, n_pop: int = 1):
+    def __init__(self, P: int, world: int, device, n_pop: int = 1, gather: bool | None = None):
+        # gather: keep a gathered buffer and exchange even at world 1 (the
+        # sharded path rehearsed on one process); default: world > 1
         self.P, self.world, self.K = int(P), int(world), int(n_pop)
+        self.sharded = bool(world > 1 if gather is None else gather)
         n = self.n = shard_capacity(P, world)
         K = self.K
         self.device = torch.device(device)
@@ -71,14 +74,17 @@ class FitnessRecords:
         self.val = (f[n:2 * n], t[n:2 * n])
         self.both = (f, t)  # per population train then validation, for one fused launch
         self.gathered = torch.zeros(world * K * record_bytes(n), dtype=torch.uint8, device=self.device) \
-            if world > 1 else None
+            if self.sharded else None
         self._host = None
 
     def all_gather(self, group=None):
         """The generation's one collective.  RCCL gathers device buffers
         directly; gloo (CPU tests, one-GPU rehearsals) goes through host memory."""
         import torch.distributed as dist
-        if self.world == 1:
+        if not self.sharded:
+            return
+        if not (dist.is_available() and dist.is_initialized()):  # one process, no group: the gather is a copy
+            self.gathered.copy_(self.rec)
             return
         if self.device.type == "cuda" and dist.get_backend(group) == "gloo":
             if self._host is None:
@@ -98,9 +104,9 @@ class FitnessRecords:
         import ctypes
         n = self.n
         lay = field_layout(n)
-        base = (self.rec if self.world == 1 else self.gathered).data_ptr()
+        base = (self.gathered if self.sharded else self.rec).data_ptr()
         ptrs = tuple(ctypes.c_void_p(base + lay[k][0]) for k in ("train_f", "train_t", "val_f", "val_t"))
-        shard = (0, 0) if self.world == 1 else (n, record_bytes(n))
+        shard = (n, record_bytes(n)) if self.sharded else (0, 0)
         return ptrs + (self.P,) + shard
 
     def multi_step_args(self):
@@ -110,17 +116,17 @@ class FitnessRecords:
         record when world == 1) and the per-population byte strides."""
         import ctypes
         n, K = self.n, self.K
-        base = (self.rec if self.world == 1 else self.gathered).data_ptr()
+        base = (self.gathered if self.sharded else self.rec).data_ptr()
         offs = (0, 16 * K * n, 8 * n, 16 * K * n + 4 * n)  # train_f, train_t, val_f, val_t
         ptrs = tuple(ctypes.c_void_p(base + o) for o in offs)
-        shard = (0, 0) if self.world == 1 else (n, K * record_bytes(n))
+        shard = (n, K * record_bytes(n)) if self.sharded else (0, 0)
         return ptrs + (16 * n, 8 * n) + shard
 
     def population(self):
         """Contiguous (train_f f64[P], train_t i32[P], val_f, val_t) of the whole
         population (torch ops; for the separate tell/val-update entry points)."""
         n, P = self.n, self.P
-        if self.world == 1:
+        if not self.sharded:
             return self.train[0][:P], self.train[1][:P], self.val[0][:P], self.val[1][:P]
         g = self.gathered.view(self.world, record_bytes(n))
         f = g[:, :16 * n].contiguous().view(torch.float64).view(self.world, 2 * n)
