@@ -161,6 +161,48 @@ __device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
     return (uint32_t)((step_off + (int64_t)kChunk * e) / kChunk);
 }
 
+// ------------------------------------------------------------------ adversary state machine
+// State (inventory, previous sell fill, previous buy fill) = 4 * inv_index + 2 fs + fb
+// (drl_engine.py:42-45, 62-63); a tick's 2-bit code is fill_buy | fill_sell << 1.
+__device__ __forceinline__ int next_state_arl(int s, int code) {
+    const int fb = code & 1, fs = code >> 1;
+    return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
+}
+
+constexpr int kArlSlot = 64;  // bytes per chunk: end state of each start state [0, 32), trades [32, 64)
+
+// One wave, lane = tick of a 64-tick chunk, fw = the lane's 2-bit fill codes
+// of every state: lanes s < ns walk the chunk from start state s and store
+// its end state and trade count -- the chunk's transducer, so the path scan
+// only chains chunk starts (the scan used to run these ns walks per chunk).
+__device__ void arl_chunk_maps(uint64_t fw, int nvalid, int ns, uint64_t* fwl, uint8_t* __restrict__ slot) {
+    const int lane = threadIdx.x & (kWave - 1);
+    fwl[lane] = lane < nvalid ? fw : 0ull;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < ns) {
+        // 8 codes per LDS round trip, then 8 register-only steps of the chain
+        // (padded ticks carry code 0: no fill, the state's flags cleared --
+        // so the walk stops at nvalid)
+        int st = lane, cnt = 0;
+        for (int t8 = 0; t8 < nvalid; t8 += 8) {
+            uint64_t f[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fwl[t8 + j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (t8 + j < nvalid) {
+                    const int c = (int)(f[j] >> (2 * st)) & 3;
+                    cnt += c != 0;
+                    st = next_state_arl(st, c);
+                }
+            }
+        }
+        slot[lane] = (uint8_t)st;
+        slot[32 + lane] = (uint8_t)cnt;
+    }
+}
+
 // ------------------------------------------------------------------ table
 // Block = 64 consecutive ticks of one episode x nsi inventory states: wave w
 // evaluates the policy and the FPT step for every tick of the block from
@@ -238,7 +280,6 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
         const double mid = spx[0][lane], ask = spx[1][lane], bid = spx[2][lane];
         const double bmax = spx[3][lane], smin = spx[4][lane];
         const int64_t row = ep.step_off[e] + t0 + lane;
-        double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
         if (!ARL) {
             const StepOut so = ftp_step(p, inv, oa, ob, mid, ask, bid, bmax, smin);
             code[w][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
@@ -250,7 +291,7 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
                 const StepOut so = ftp_step(p, inv, oa + lut[0][s], ob + lut[1][s], mid, ask,
                                             bid, bmax, smin);
                 code[s][lane] = (uint8_t)(so.fill_buy | (so.fill_sell << 1));
-                R[s] = so.reward;
+                rew[s * ep.rs + row] = so.reward;  // per-state planes (SoA): coalesced rows
             }
         }
     }
@@ -258,11 +299,12 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     if (w != 0) return;
     const int64_t row = ep.step_off[e] + t0 + lane;
     if (ARL) {
-        if (valid) {
-            uint64_t fw = 0;
-            for (int s = 0; s < ns; ++s) fw |= (uint64_t)code[s][lane] << (2 * s);
-            fills[row] = fw;
-        }
+        uint64_t fw = 0;
+        for (int s = 0; s < ns; ++s) fw |= (uint64_t)code[s][lane] << (2 * s);
+        if (valid) fills[row] = fw;
+        __shared__ uint64_t fwl[kWave];
+        arl_chunk_maps(fw, nvalid, ns, fwl,
+                       reinterpret_cast<uint8_t*>(cmaps) + (int64_t)(chunk_base(ep.step_off[e], e) + blockIdx.x) * kArlSlot);
         return;
     }
     uint64_t map = kIdentityMap;
@@ -523,7 +565,6 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
     asm volatile("" ::: "memory");
     if (valid) {
         const double mid = tmid, ask = task, bid = tbid, bmax = tbmax, smin = tsmin;
-        double* __restrict__ R = rew + row * ns;  // adversary rows (AoS)
 #pragma unroll
         for (int si = 0; si < NSI; ++si) {
             if (si >= nsi) break;
@@ -543,13 +584,16 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
                     const StepOut so = ftp_step(p, inv, oa + lut0[s], ob + lut1[s], mid, ask, bid,
                                                 bmax, smin);
                     fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * s);
-                    R[s] = so.reward;
+                    rew[s * ep.rs + row] = so.reward;  // per-state planes (SoA): coalesced rows
                 }
             }
         }
     }
     if (ARL) {
         if (valid) fills[row] = fw;
+        __shared__ uint64_t fwl_s[4][kWave];
+        arl_chunk_maps(fw, min(kChunk, T - t0), ns, fwl_s[threadIdx.x >> 6],
+                       reinterpret_cast<uint8_t*>(cmaps) + (int64_t)(chunk_base(ep.step_off[e], e) + chunk) * kArlSlot);
         return;
     }
     SGMM_TSTAMP(wslot, 3, map + traded);
@@ -1688,15 +1732,21 @@ __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __re
 // 20-state transducer (inventory x previous fills): every chunk is walked from
 // every start state, the chunk end-maps are chained, each chunk is replayed
 // from its true start.  Dynamic LDS: [kSeg doubles][nch*ns end maps][nch starts]
-__device__ __forceinline__ int next_state_arl(int s, int code) {
-    const int fb = code & 1, fs = code >> 1;
-    return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
-}
-
 __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
-    const uint64_t* __restrict__ fills, const double* __restrict__ rew,
+    const uint64_t* __restrict__ fills, const uint8_t* __restrict__ chunks, const double* __restrict__ rew,
     double* __restrict__ fitness, int32_t* __restrict__ trades_out, StepArgs step) {
+    // chunks: per 64-tick chunk the table's transducer (end state and trade
+    // count from each of the ns start states, kArlSlot bytes); rew: per-state
+    // reward planes rew[s * rs + row].  Per episode:
+    //   1. the chunks' start states: the end maps chained by pointer jumping
+    //      (log2(chunks) rounds over all (chunk, state) pairs, no serial lane),
+    //      trades = the sum of every chunk's count from its start state;
+    //   2. per 4096-tick segment, one thread per chunk walks its 64 ticks
+    //      from the start state with the fill codes and gathers the rewards
+    //      from the per-state planes (consecutive ticks of one state are
+    //      consecutive addresses);
+    //   3. the exact sequential float64 sum.
     extern __shared__ __align__(16) unsigned char lds[];
     double* sel = reinterpret_cast<double*>(lds);
     __shared__ SumLds<kScanBlock> L;
@@ -1704,32 +1754,39 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     const int32_t T = ep.len[e];
     const int ns = 4 * nsi;
     const int nch = (T + kChunk - 1) / kChunk;
-    uint8_t* endmap = lds + kSeg * sizeof(double);
-    uint8_t* start = endmap + nch * ns;
+    uint8_t* jm = lds + kSeg * sizeof(double);   // [2][nch][ns] jump maps (double-buffered)
+    uint8_t* start = jm + 2 * nch * ns;          // [nch]
     __shared__ int red_trades;
     const int64_t so = ep.step_off[e];
     const uint64_t* __restrict__ F = fills + so;
-    const double* __restrict__ R = rew + so * ns;
+    const uint8_t* __restrict__ C = chunks + (int64_t)chunk_base(so, e) * kArlSlot;
     const int tid = threadIdx.x;
     if (tid == 0) red_trades = 0;
-    for (int i = tid; i < nch * ns; i += kScanBlock) {
-        const int k = i / ns;
-        int s = i - k * ns;
-        const int ta = k * kChunk, tb = min(T, ta + kChunk);
-        for (int t = ta; t < tb; ++t) s = next_state_arl(s, (int)(F[t] >> (2 * s)) & 3);
-        endmap[i] = (uint8_t)s;
-    }
+    // jm[k][s] = state after chunks k-2^r+1 .. k from state s at chunk k-2^r+1's start
+    for (int i = tid; i < nch * ns; i += kScanBlock) jm[i] = C[(i / ns) * kArlSlot + i % ns];
     __syncthreads();
-    if (tid == 0) {
-        int s = (-inv_min) << 2;
-        for (int k = 0; k < nch; ++k) {
-            start[k] = (uint8_t)s;
-            s = endmap[k * ns + s];
+    int cur = 0;
+    for (int d = 1; d < nch; d <<= 1) {
+        const uint8_t* a = jm + cur * nch * ns;
+        uint8_t* b = jm + (cur ^ 1) * nch * ns;
+        for (int i = tid; i < nch * ns; i += kScanBlock) {
+            const int k = i / ns, st = i - k * ns;
+            b[i] = k >= d ? a[k * ns + a[(k - d) * ns + st]] : a[i];
         }
+        cur ^= 1;
+        __syncthreads();
+    }
+    // start of chunk k = inclusive prefix of chunks 0 .. k-1 applied to the episode start
+    const int s0 = (-inv_min) << 2;
+    const uint8_t* pre = jm + cur * nch * ns;
+    int my_trades = 0;
+    for (int k = tid; k < nch; k += kScanBlock) {
+        const int st = k == 0 ? s0 : pre[(k - 1) * ns + s0];
+        start[k] = (uint8_t)st;
+        my_trades += C[k * kArlSlot + 32 + st];
     }
     __syncthreads();
     double total = 0.0;
-    int my_trades = 0;
     for (int seg0 = 0; seg0 < T; seg0 += kSeg) {
         const int segn = min(kSeg, T - seg0);
         const int segch = (segn + kChunk - 1) / kChunk;
@@ -1739,8 +1796,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
             const int ta = k * kChunk, tb = min(T, ta + kChunk);
             for (int t = ta; t < tb; ++t) {
                 const int code = (int)(F[t] >> (2 * s)) & 3;
-                sel[t - seg0] = R[(int64_t)t * ns + s];
-                my_trades += (code != 0);
+                sel[t - seg0] = rew[(int64_t)s * ep.rs + so + t];
                 s = next_state_arl(s, code);
             }
         }
@@ -2012,8 +2068,9 @@ static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(u
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
                                               int32_t n_states) {
     if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
-    if (n_states > 8)  // adversary: rew[row * n_states + state]
-        return ws_fills(total_steps) + align256((size_t)total_steps * (size_t)n_states * sizeof(double));
+    if (n_states > 8)  // adversary: fill codes, chunk transducers, per-state planes rew[state * rs + row]
+        return ws_fills(total_steps) + align256(n_chunk_slots(n_episodes, total_steps) * kArlSlot) +
+               (size_t)rew_stride(total_steps, n_episodes) * (size_t)n_states * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
            (size_t)rew_stride(total_steps, n_episodes) * (size_t)n_states * sizeof(double);
 }
@@ -2150,7 +2207,9 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
-        rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
+        cmaps = reinterpret_cast<uint64_t*>(w + ws_fills(eps->total_steps));  // chunk transducers
+        rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps) +
+                                        align256(n_chunk_slots(eps->n, eps->total_steps) * kArlSlot));
     } else {
         const size_t a = ws_cmaps(eps->n, eps->total_steps), b = ws_ctr(eps->n, eps->total_steps);
         cmaps = reinterpret_cast<uint64_t*>(w);
@@ -2201,10 +2260,10 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     const int nch_max = (eps->max_len + kChunk - 1) / kChunk;
     ProfScope prof("path_scan", s);
     if (arl) {
-        size_t lds = kSeg * sizeof(double) + (size_t)nch_max * ns + nch_max;
+        size_t lds = kSeg * sizeof(double) + (size_t)2 * nch_max * ns + nch_max;
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanBlock, step));
-        SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params,
-                           eps->inv_min, nsi, fills, rew, fitness, trades, step);
+        SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params, eps->inv_min, nsi,
+                    fills, reinterpret_cast<const uint8_t*>(cmaps), rew, fitness, trades, step);
     } else {
         // the workgroup shrinks as episodes grow: few episodes get a 16-wave
         // workgroup each (4096-tick windows, the phases spread over the CU);

@@ -71,8 +71,9 @@ def test_argument_errors_need_no_gpu(sgmm):
     rc = L.sgmm_bar_windows(ctypes.byref(ev), 1, ctypes.c_void_p(8), ctypes.c_void_p(8), ctypes.c_void_p(8),
                             ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
     assert rc == -1 and b"bars per day" in L.sgmm_last_error()
-    # adversary (20 states): u64 fill words + f64 rewards
-    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 160000
+    # adversary (20 states): u64 fill words + 64-byte chunk transducers (1000/64 + 4 + 1 slots)
+    # + per-state f64 reward planes (stride 1000 + 256 * 4 rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 2048 * 8
 
 
 def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):
