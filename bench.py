@@ -303,7 +303,8 @@ def main():
                    "training tick on this workload, in 16-lane MFMA tiles)" if kname == "policy_frontier" else
                    "k_policy_table_v3 evaluates every inventory state (5x this work)"))
         roofline = {"bound": "mfma", "pipe": "fp32 (gfx950 f32 MFMA peak == f32 VALU peak)",
-                    "kernel": "k_policy_frontier" if kname == "policy_frontier" else "k_policy_table_v3",
+                    "kernel": ("k_policy_frontier" if kname == "policy_frontier" else
+                               "k_policy_table_mfma (adversary)" if spec["arl"] else "k_policy_table_v3"),
                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                     "algorithmic": {"flop_per_env_step": fl, "env_steps_per_launch": steps_per_launch,
