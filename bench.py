@@ -3,11 +3,15 @@
 
 One step = one GA generation of every population on every GPU:
   ask (population from master + sigma * N(0,1), generated inside the rollout)
-  -> rollout of the populations' training episodes (+ fused validation
-     episodes of the same genomes)
+  -> rollout of the populations' training episodes
   -> [N > 1: one RCCL all-gather of the fitness records]
-  -> tell (argmax, new master) -> validation bookkeeping / sigma decay,
-run through MultiDRLEngine (K populations in one launch pair per generation).
+  -> tell (argmax, new master) -> validation of each population's new master
+     (one episode per population, the reference's order) -> validation
+     bookkeeping / sigma decay,
+run through MultiDRLEngine (K populations in the same launches).  With
+--val-mode fused (the default below 256 individuals per population) every
+individual's validation episode runs inside the training launch instead and
+the tail picks the best's (two launches per generation).
 value = training env-steps (population x training ticks, all populations,
 all ranks) per generation / measured seconds per generation; validation ticks
 are executed but not counted.
@@ -79,6 +83,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-episodes", type=int, default=64, help="episodes in the CPU-baseline sample")
     ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest for this config)")
+    ap.add_argument("--val-mode", default="auto", choices=("auto", "fused", "best"),
+                    help="DRLEngine val_mode (auto: best from 256 individuals per population shard)")
     return ap.parse_args()
 
 
@@ -114,7 +120,7 @@ def bundles(spec, seed=0):
     return out
 
 
-def describe(spec, world, P_glob):
+def describe(spec, world, P_glob, best_val):
     pops = spec["pops"]
     H = spec["H"]
     cfg_match = {k: v for k, v in CONFIGS.items()
@@ -124,7 +130,8 @@ def describe(spec, world, P_glob):
     lam = ", ".join(f"phi={p} tick={t} {a}" for p, t, a in pops)
     return (head + f"{len(pops)} GA population(s) x {P_glob} individuals ({lam}), "
             f"TradingPolicy 3->{H}->{H}->2{' + AdversaryPolicy pairs' if spec['arl'] else ''}, synthetic ticks "
-            f"({spec['T']} train + {spec['Tv']} fused validation), {world} GPU(s), "
+            f"({spec['T']} train + {spec['Tv']} validation: "
+            f"{'the new master of each population' if best_val else 'every individual, fused'}), {world} GPU(s), "
             f"{spec['scaling']} scaling")
 
 
@@ -196,12 +203,12 @@ def latest_pmc(path_arg, config):
         return None
 
 
-def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, seed0=1234):
+def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, val_mode, seed0=1234):
     import torch
     torch.manual_seed(seed0)
     engines = [sgmm.DRLEngine(pop_size=P_glob, phi=phi, tick_size=tick, fee_rate=0.0, use_arl=spec["arl"],
                               save_dir=save_dir, hidden_dim=spec["H"], rng="device", seed=seed0 + 17 * k,
-                              val_mode="fused", sync_every=10**9, verbose=False, use_graph=use_graph, dist=dist)
+                              val_mode=val_mode, sync_every=10**9, verbose=False, use_graph=use_graph, dist=dist)
                for k, (phi, tick, _) in enumerate(spec["pops"])]
     return sgmm.MultiDRLEngine(engines)
 
@@ -243,7 +250,7 @@ def main():
             dist.barrier()
 
     tmp = tempfile.mkdtemp(prefix="sgmm_bench_")
-    eng = make_engine(sgmm, spec, P_glob, tmp, None, not args.no_graph)
+    eng = make_engine(sgmm, spec, P_glob, tmp, None, not args.no_graph, args.val_mode)
     sess = eng.session(tr, va, st, generations=args.warmup + args.steps)
     sess.steps(0, args.warmup)
     sess.capture()  # graphs recorded (not run) before the timed region
@@ -269,7 +276,7 @@ def main():
     # dispatch on the launch stream (hipExtLaunchKernel, sgmm_profile_*); graph
     # replays launch the identical kernels
     n_rank = shard_capacity(P_glob, world)
-    peng = make_engine(sgmm, spec, n_rank, tmp, False, False, seed0=99)
+    peng = make_engine(sgmm, spec, n_rank, tmp, False, False, args.val_mode, seed0=99)
     psess = peng.session(tr, va, st, generations=args.profile_steps + 2)
     psess.step(0)
     psess.step(1)
@@ -287,7 +294,9 @@ def main():
 
     # roofline of the policy kernel (the FP32 compute kernel of the path): the
     # frontier kernel from 2048 episodes per launch, the table below that
-    steps_per_launch = K * n_rank * (T + Tv)  # fused validation: train + validation episodes
+    best_val = bool(sess.best_val)
+    # the training launch: training episodes (+ every validation episode when fused)
+    steps_per_launch = K * n_rank * (T if best_val else T + Tv)
     fl = flop_per_step(H)
     kname = "policy_frontier" if "policy_frontier" in kernels else "policy_table"
     tab = kernels.get(kname)
@@ -298,7 +307,8 @@ def main():
         traffic = None
         if pmc and pmc.get("kernels", {}).get(kname):
             traffic = pmc["kernels"][kname].get("hbm_bytes_per_launch")
-        note = ("algorithmic = one policy forward per env-step (train + validation ticks of one launch). "
+        note = ("algorithmic = one policy forward per env-step ("
+                + ("training" if best_val else "training + validation") + " ticks of one launch). "
                 + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.35 per "
                    "training tick on this workload, in 16-lane MFMA tiles)" if kname == "policy_frontier" else
                    "k_policy_table_v3 evaluates every inventory state (5x this work)"))
@@ -323,10 +333,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": spec["scaling"], "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
-            "config": {"workload": describe(spec, world, P_glob), "config_id": args.config,
+            "config": {"workload": describe(spec, world, P_glob, best_val), "config_id": args.config,
                        "populations": K, "population_global": P_glob, "population_per_gpu": n_rank,
                        "phis": [p for p, _, _ in spec["pops"]], "hidden": H, "ticks_train": T, "ticks_val": Tv,
-                       "adversary": spec["arl"], "val_mode": "fused",
+                       "adversary": spec["arl"], "val_mode": "best" if best_val else "fused",
                        "parallelism": f"population shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
                        "hip_graph": bool(sess.use_graph),
                        "graph_has_exchange": bool(sess.full_graph) if world > 1 else None,

@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading libsgmm.so, see module doc)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("SGMM_LIB", PKG_DIR / "libsgmm.so"))
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class SgmmError(RuntimeError):
@@ -129,6 +129,12 @@ SIGNATURES = {
                                                         ctypes.c_size_t, _VP]),
     "sgmm_ga_step_multi": (ctypes.c_int, [ctypes.POINTER(Populations), _VP, _VP, _VP, _VP, _I64, _I64, _I32,
                                           _I64, _VP]),
+    "sgmm_generation_multi_best": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes),
+                                                  ctypes.POINTER(Episodes), _VP, ctypes.POINTER(Populations),
+                                                  _VP, _VP, _VP, _VP, _VP, ctypes.c_size_t, _VP]),
+    "sgmm_validate_multi": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
+                                           ctypes.POINTER(Populations), _VP, _VP, _VP, ctypes.c_size_t, _VP]),
+    "sgmm_ga_tell_multi": (ctypes.c_int, [ctypes.POINTER(Populations), _VP, _VP, _I64, _I64, _I32, _I64, _VP]),
     "sgmm_event_bars_workspace_size": (ctypes.c_size_t, [_I64]),
     "sgmm_event_bars_build": (ctypes.c_int, [ctypes.POINTER(DayStreams), ctypes.POINTER(EventBars), _VP,
                                              ctypes.c_size_t, _VP]),

@@ -19,13 +19,23 @@ namespace sgmm {
 
 constexpr int kWave = 64;
 
-// ReLU on the float's bit pattern: max(bits, 0) as a signed integer (one
-// v_max_i32, no NaN canonicalisation).  Equals torch's relu for every
-// non-NaN input (-0.0 -> +0.0); a NaN keeps its payload if positive and becomes
-// 0 if negative -- NaN only arises from NaN state inputs, where the
-// reference's own action cast (NaN -> int) is undefined anyway.
+// ReLU as one v_med3_f32(a, 0, +inf) on the float pipe.  +inf goes through an
+// empty asm (opaque to the optimizer, hoisted once per kernel): a visible
+// med3(a, 0, inf) is folded into max(a, 0), and max of an MFMA result gets an
+// extra canonicalising v_max per value.  Not the integer max on the bit
+// pattern: while another wave of the SIMD streams MFMAs, integer VALU ops
+// issue at half rate and float ops at full rate (tools/mb/mb_mfma_xwave2.hip).
+// Equals torch's relu for every non-NaN input (-0.0 -> +0.0 up to the sign of
+// an exact zero, which no action depends on); NaN pre-activations (NaN state
+// inputs only) are outside the parity domain (oracle/sgmm_oracle.c relu32).
 __device__ __forceinline__ float relu(float a) {
+#ifdef SGMM_RELU_INT  // A/B builds only: round 1's integer max on the bit pattern
     return __int_as_float(max(__float_as_int(a), 0));
+#else
+    float pinf = __builtin_inff();
+    asm("" : "+s"(pinf));
+    return __builtin_amdgcn_fmed3f(a, 0.0f, pinf);
+#endif
 }
 
 // float -> int action: saturating, NaN -> INT32_MIN (the x86 cvtt value numpy's

@@ -114,38 +114,9 @@ __global__ __launch_bounds__(kTellBlock) void k_ga_val_update(
     float* __restrict__ best_master, int64_t n, sgmm_ga_history* __restrict__ history,
     int32_t hist_cap) {
     __shared__ int improved;
-    sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
     const int idx = use_best ? st->best_idx : 0;
-    const double v = vfit[idx];
-    if (threadIdx.x == 0) improved = v > st->best_val;  // drl_engine.py:143 (NaN -> False)
-    __syncthreads();
-    if (improved && best_master)
-        for (int64_t k = threadIdx.x; k < n; k += kTellBlock) best_master[k] = master[k];
-    if (threadIdx.x == 0) {
-        int decayed = 0;
-        if (improved) {
-            st->best_val = v;
-            st->no_improve = 0;
-        } else {
-            st->no_improve += 1;
-        }
-        if (st->no_improve >= st->patience) {  // drl_engine.py:155-160
-            st->sigma_mm *= st->decay;
-            st->sigma_adv *= st->decay;
-            st->no_improve = 0;
-            decayed = 1;
-        }
-        st->improved = improved;
-        st->decayed = decayed;
-        st->last_val_f = v;
-        st->gen += 1;
-        if (hist) {
-            hist->val_f = v;
-            hist->val_trades = vtrades ? vtrades[idx] : 0;
-            hist->sigma_after = st->sigma_mm;
-            hist->flags = improved | (decayed << 1);
-        }
-    }
+    val_update_dev(st, vfit[idx], vtrades ? vtrades[idx] : 0, master, best_master, n, history, hist_cap,
+                   &improved);
 }
 
 __global__ void k_ga_state_init(sgmm_ga_state* st, double sigma, int32_t patience, double decay) {
@@ -203,7 +174,7 @@ __device__ __forceinline__ const T* at_bytes(const T* p, int64_t off) {
 __global__ __launch_bounds__(kStepBlock) void k_ga_step_multi(
     PopsArg pa, const double* __restrict__ fit, const int32_t* __restrict__ trades,
     const double* __restrict__ vfit, const int32_t* __restrict__ vtrades, int64_t fit_ps,
-    int64_t tr_ps, ShardView shard) {
+    int64_t tr_ps, ShardView shard, int tell_only) {
     __shared__ double sv[2 * kStepBlock];
     __shared__ int si[2 * kStepBlock];
     __shared__ float lm[kMaxStepParams];
@@ -214,7 +185,7 @@ __global__ __launch_bounds__(kStepBlock) void k_ga_step_multi(
                        pa.masters_mm + k * pa.n_mm, pa.masters_adv ? pa.masters_adv + k * pa.n_adv : nullptr,
                        pa.best_masters ? pa.best_masters + k * pa.n_mm : nullptr, pa.n_mm, pa.n_adv, pa.seeds[k],
                        pa.history ? pa.history + (int64_t)k * pa.hist_cap : nullptr, pa.hist_cap, nullptr,
-                       nullptr, 0, 0, sv, si, lm, la);
+                       nullptr, 0, 0, sv, si, lm, la, tell_only != 0);
 }
 
 }  // namespace sgmm
@@ -237,7 +208,27 @@ extern "C" int sgmm_ga_step_multi(const sgmm_populations* pops, const double* fi
     ProfScope prof("ga_step", as_stream(stream));
     hipLaunchKernelGGL(k_ga_step_multi, dim3(pops->n_pop), dim3(kStepBlock), 0, as_stream(stream), pa,
                        fitness, trades, val_fitness, val_trades, fit_pop_stride, trades_pop_stride,
-                       ShardView{shard_n, shard_stride});
+                       ShardView{shard_n, shard_stride}, 0);
+    SGMM_LAUNCHED();
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_ga_tell_multi(const sgmm_populations* pops, const double* fitness, const int32_t* trades,
+                                  int64_t fit_pop_stride, int64_t trades_pop_stride, int32_t shard_n,
+                                  int64_t shard_stride, void* stream) {
+    clear_error();
+    SGMM_REQUIRE(pops && pops->n_pop > 0 && pops->P > 0, "bad populations");
+    SGMM_REQUIRE(supported_hidden(pops->hidden), "hidden=%d unsupported", pops->hidden);
+    SGMM_REQUIRE(pops->states && pops->masters_mm && pops->seeds && fitness, "null pointer");
+    SGMM_REQUIRE(shard_n <= 0 || shard_stride >= 8LL * shard_n, "shard_stride < 8 * shard_n");
+    const int64_t n_mm = (int64_t)pops->hidden * pops->hidden + 7 * pops->hidden + 2;
+    SGMM_REQUIRE(n_mm <= kMaxStepParams, "genome too large for the GA step");
+    PopsArg pa{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, pops->seeds,
+               pops->history, pops->history_cap, pops->P, n_mm, pops->masters_adv ? 1250 : 0};
+    ProfScope prof("ga_tell", as_stream(stream));
+    hipLaunchKernelGGL(k_ga_step_multi, dim3(pops->n_pop), dim3(kStepBlock), 0, as_stream(stream), pa,
+                       fitness, trades, nullptr, nullptr, fit_pop_stride, trades_pop_stride,
+                       ShardView{shard_n, shard_stride}, 1);
     SGMM_LAUNCHED();
     return SGMM_OK;
 }

@@ -153,6 +153,74 @@ __device__ void ask_rows(const float* lds_master, int64_t n, float sig, uint64_t
     }
 }
 
+// The tell's bookkeeping when the validation runs after it (reference order,
+// drl_engine.py:119-128): best / adversary indices, the best training record,
+// the history row's training fields.  One thread.
+template <bool HANDOFF>
+__device__ __forceinline__ void tell_record(sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
+                                            const int32_t* __restrict__ trades, ShardView shard, int best,
+                                            int abest, sgmm_ga_history* __restrict__ hist) {
+    const double tf = shard_ld<HANDOFF>(fit, shard, best);
+    const int32_t ttr = trades ? shard_ld<HANDOFF>(trades, shard, best) : 0;
+    st->best_idx = best;
+    st->adv_best_idx = abest;
+    st->last_train_f = tf;
+    if (hist) {
+        hist->train_f = tf;
+        hist->train_trades = ttr;
+        hist->best_idx = best;
+    }
+}
+
+// Validation bookkeeping of one population (drl_engine.py:129-160): v / vtr
+// are the validation record of the post-tell master.  Checkpoint copy
+// master -> best_master on improvement (strictly greater; NaN never improves),
+// sigma decay after `patience` generations without improvement, the history
+// row's validation fields, gen + 1.  Every thread of the workgroup calls
+// (v identical in all); `flag` is one int of LDS scratch.
+__device__ __forceinline__ void val_update_dev(sgmm_ga_state* __restrict__ st, double v, int32_t vtr,
+                                               const float* __restrict__ master, float* __restrict__ best_master,
+                                               int64_t n, sgmm_ga_history* __restrict__ history,
+                                               int32_t hist_cap, int* flag) {
+    if (threadIdx.x == 0) {
+        const int32_t gen = st->gen;
+        sgmm_ga_history* hist = (history && gen < hist_cap) ? history + gen : nullptr;
+        const int improved = v > st->best_val;
+        int decayed = 0;
+        int32_t no_improve = st->no_improve;
+        if (improved) {
+            st->best_val = v;
+            no_improve = 0;
+        } else {
+            no_improve += 1;
+        }
+        double smm = st->sigma_mm, sadv = st->sigma_adv;
+        if (no_improve >= st->patience) {  // drl_engine.py:155-160
+            smm *= st->decay;
+            sadv *= st->decay;
+            no_improve = 0;
+            decayed = 1;
+        }
+        st->sigma_mm = smm;
+        st->sigma_adv = sadv;
+        st->no_improve = no_improve;
+        st->improved = improved;
+        st->decayed = decayed;
+        st->last_val_f = v;
+        st->gen = gen + 1;
+        if (hist) {
+            hist->val_f = v;
+            hist->val_trades = vtr;
+            hist->sigma_after = smm;
+            hist->flags = improved | (decayed << 1);
+        }
+        *flag = improved;
+    }
+    __syncthreads();
+    if (*flag && best_master)
+        for (int64_t k = threadIdx.x; k < n; k += blockDim.x) best_master[k] = master[k];
+}
+
 // One generation boundary, executed by one whole workgroup (power-of-two
 // size): tell both evolvers, validation bookkeeping, sigma decay, history
 // row, and optionally the next generation's ask of [i0, i0+n).
@@ -167,7 +235,7 @@ __device__ void ga_step_dev(sgmm_ga_state* __restrict__ st, const double* __rest
                             float* __restrict__ best_master, int64_t n_mm, int64_t n_adv,
                             uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap,
                             float* __restrict__ next_mm, float* __restrict__ next_adv, int32_t i0,
-                            int32_t n, double* sv, int* si, float* lm, float* la) {
+                            int32_t n, double* sv, int* si, float* lm, float* la, bool tell_only = false) {
     const int tid = threadIdx.x, nt = blockDim.x;
     const uint32_t gen = (uint32_t)st->gen;
     sgmm_ga_history* hist = (history && st->gen < hist_cap) ? history + st->gen : nullptr;
@@ -178,6 +246,10 @@ __device__ void ga_step_dev(sgmm_ga_state* __restrict__ st, const double* __rest
     // tell (model.py:73-76; drl_engine.py:119-125)
     regen_master(master, lm, n_mm, sig_mm, seed, 0u, gen, best);
     if (master_adv) regen_master(master_adv, la, n_adv, sig_adv, seed, 1u, gen, abest);
+    if (tell_only) {  // the validation of the new master follows in its own launches
+        if (tid == 0) tell_record<HANDOFF>(st, fit, trades, shard, best, abest, hist);
+        return;
+    }
     if (tid == 0) {
         // validation of the best (drl_engine.py:129-171); every load issued
         // before the first dependent use
@@ -307,7 +379,7 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
                               float* __restrict__ master, float* __restrict__ master_adv,
                               float* __restrict__ best_master, int64_t n_mm, int64_t n_adv,
                               uint64_t seed, sgmm_ga_history* __restrict__ history, int32_t hist_cap,
-                              double* sv, int* si, float* lm, float* la) {
+                              double* sv, int* si, float* lm, float* la, bool tell_only = false) {
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int nw = (nt + kWave - 1) / kWave;
     // ---- every load first
@@ -316,9 +388,9 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
     const bool mine = tid < P;
     if (mine) {
         f = ld_rec<HANDOFF>(fit + tid);
-        vf = ld_rec<HANDOFF>(vfit + tid);
+        if (!tell_only) vf = ld_rec<HANDOFF>(vfit + tid);
         if (trades) tr = ld_rec<HANDOFF>(trades + tid);
-        if (vtrades) vtr = ld_rec<HANDOFF>(vtrades + tid);
+        if (vtrades && !tell_only) vtr = ld_rec<HANDOFF>(vtrades + tid);
     }
     float mm[kTailSlots][4], ma[kTailSlots][4];
     load_master4(master, n_mm, mm);
@@ -374,13 +446,27 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
     }
     const int best = bi, abest = aj;
     // every thread knows whether the validation improved (drl_engine.py:130-131)
-    const int improved = pv > best_val;
+    const int improved = !tell_only && pv > best_val;
     SGMM_TAIL_STAMP(1, best + abest);
     // ---- tell (model.py:73-76; drl_engine.py:119-125), the checkpoint copy
     // of the new master written in the same pass
     regen_master_regs(master, improved ? best_master : nullptr, n_mm, mm, sig_mm, seed, 0u, gen, best);
     if (master_adv) regen_master_regs(master_adv, nullptr, n_adv, ma, sig_adv, seed, 1u, gen, abest);
     SGMM_TAIL_STAMP(2, mm[0][0]);
+    if (tell_only) {  // the validation of the new master follows in its own launches
+        if (tid == 0) {
+            st->best_idx = best;
+            st->adv_best_idx = abest;
+            st->last_train_f = bv;
+            if (history && gen_i < hist_cap) {
+                sgmm_ga_history* hist = history + gen_i;
+                hist->train_f = bv;
+                hist->train_trades = pt;
+                hist->best_idx = best;
+            }
+        }
+        return;
+    }
     if (tid == 0) {  // validation of the best (drl_engine.py:129-171)
         const double v = pv, tf = bv;
         double smm = st_smm, sadv = st_sadv;

@@ -964,8 +964,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #ifdef SGMM_STAMPS_PHASE
     // per wave (episode): 0 cycles, 1 tile-slots, 2 slots, 3 layer 1-3 cycles,
     // 4 FPT-step cycles, 5 per-tick head (frontier, signals, layer-1 terms), 6 planes
-    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0};
+    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
 #define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
     SGMM_FT(fs_t0);
 #endif
     int64_t ti = tick_of(0);
@@ -1173,12 +1174,16 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         unsigned long long t_;
         SGMM_FT(t_);
         fs_c[0] = t_ - fs_t0;
-        if (lane == 0 && e < kStampWaves)
+        unsigned long long r1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+        if (lane == 0 && e < kStampWaves) {
             for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
+            g_tstamps[e][7] = r1 - fs_r0;  // wall time in 10 ns ticks: the shader clock = [0] / [7]
+        }
     }
 #undef SGMM_FT
 #endif
-#ifdef SGMM_STAMPS
+#if defined(SGMM_STAMPS) && !defined(SGMM_STAMPS_PHASE)
     {
         unsigned long long t1;
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
@@ -1538,6 +1543,11 @@ struct StepArgs {
     // fitness + k * pop_eps.  pop_eps == 0: one population (the whole grid).
     int32_t pop_eps;
     const uint64_t* seeds;
+    // 0: the whole boundary (records: P training then P validation results per
+    // population); 1: tell only (the validation of the new master follows in its
+    // own launches); 2: validation bookkeeping, one episode per population
+    // (workgroup k = population k's post-tell master, validation_tail)
+    int32_t mode;
 };
 
 // LDS bytes the tail needs (aliased onto the kernel's dynamic LDS)
@@ -1593,16 +1603,28 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
     int* si = reinterpret_cast<int*>(sv + 2 * nt);
     float* lm = reinterpret_cast<float*>(si + 2 * nt);
     float* la = lm + sa.n_mm;
+    const bool tell_only = sa.mode == 1;
     if (sa.P <= nt && sa.n_mm <= 16 * nt && sa.n_adv <= 16 * nt)
         ga_step_fused<true>(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, sa.master_mm,
                             sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed, sa.history,
-                            sa.hist_cap, sv, si, lm, la);
+                            sa.hist_cap, sv, si, lm, la, tell_only);
     else
         ga_step_dev<true>(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, ShardView{0, 0},
                           sa.master_mm, sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed,
-                          sa.history, sa.hist_cap, nullptr, nullptr, 0, 0, sv, si, lm, la);
+                          sa.history, sa.hist_cap, nullptr, nullptr, 0, 0, sv, si, lm, la, tell_only);
     if (threadIdx.x == 0) sa.st->arrivals = 0;
     SGMM_STAMP(blockIdx.x, 5);
+}
+
+// The validation launch's tail (StepArgs::mode 2): workgroup k holds the
+// validation record (v, vtr: thread 0's values) of population k's post-tell
+// master and runs its bookkeeping -- no other workgroup's record is needed.
+__device__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag) {
+    const int k = blockIdx.x;
+    __syncthreads();  // flag aliases LDS the caller has just read
+    val_update_dev(sa.st + k, v, vtr, sa.master_mm + (int64_t)k * sa.n_mm,
+                   sa.best_master ? sa.best_master + (int64_t)k * sa.n_mm : nullptr, sa.n_mm,
+                   sa.history ? sa.history + (int64_t)k * sa.hist_cap : nullptr, sa.hist_cap, flag);
 }
 
 // ------------------------------------------------------------------ path scan (no adversary)
@@ -1702,13 +1724,17 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
         S = exact_sum_window<NT>(sel, n, S, L);
     }
     SGMM_STAMP(e, 3);
+    int tr = 0;  // thread 0's record (the tails read it there only)
+    double total = S;
     if (tid == 0) {
-        const int tr = red_trades;
-        double total = S;
+        tr = red_trades;
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
         store_record(fitness, trades_out, e, total, tr);
     }
-    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
+    if (step.st) {
+        if (step.mode == 2) validation_tail(step, total, tr, &red_trades);
+        else generation_tail(step, fitness, trades_out, lds, &red_trades);
+    }
 }
 
 // ------------------------------------------------------------------ ordered sum (standalone)
@@ -2219,10 +2245,11 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     const EpArrays ep = ep_arrays(eps, arl);
     const bool fr = use_frontier(arl, hidden, eps);
+    const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
     if (fr && eps->max_len > 0) {
-        ProfScope prof("policy_frontier", s);
+        ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
         const dim3 grid(eps->n), block(kWave);
 #define SGMM_FRONTIER(H_, NSI_)                                                                            \
     SGMM_LAUNCH((k_policy_frontier<H_, NSI_>), grid, block, 0, s, *ticks, ep, params, src, eps->inv_min, nsi, \
@@ -2238,7 +2265,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         SGMM_LAUNCHED();
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
-        ProfScope prof("policy_table", s);
+        ProfScope prof(vt ? "val_policy_table" : "policy_table", s);
         const bool valu = table_path() == 1;
         switch (hidden) {
             case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew); break;
@@ -2258,7 +2285,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         SGMM_LAUNCHED();
     }
     const int nch_max = (eps->max_len + kChunk - 1) / kChunk;
-    ProfScope prof("path_scan", s);
+    ProfScope prof(vt ? "val_path_scan" : "path_scan", s);
     if (arl) {
         size_t lds = kSeg * sizeof(double) + (size_t)2 * nch_max * ns + nch_max;
         if (step.st) lds = std::max(lds, step_lds_bytes(kScanBlock, step));
@@ -2375,6 +2402,65 @@ extern "C" int sgmm_generation_multi(const sgmm_ticks* ticks, const sgmm_episode
                   pops->history, pops->history_cap, P, 2 * P, pops->seeds};
     return rollout_impl(ticks, eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes, step,
                         as_stream(stream));
+}
+
+// Validation of every population's post-tell master (drl_engine.py:129-160):
+// val_eps episode k runs masters_mm row val_eps->genome[k] (= k) with no
+// adversary; the scan's workgroup k then runs population k's validation
+// bookkeeping (validation_tail).  The policy kernel is the table (K episodes).
+static int validate_impl(const sgmm_ticks* ticks, const sgmm_episodes* val_eps, const sgmm_env_params* params,
+                         const sgmm_populations* pops, double* val_fitness, int32_t* val_trades, void* workspace,
+                         size_t workspace_bytes, hipStream_t s) {
+    const int32_t H = pops->hidden, K = pops->n_pop;
+    if (int rc = check_episodes(ticks, val_eps, params, pops->masters_mm, H)) return rc;
+    SGMM_REQUIRE(val_eps->n == K, "validation episodes must be one per population (%d), got %d", K, val_eps->n);
+    const int64_t n_mm = (int64_t)H * H + 7 * H + 2;
+    const GenomeSrc src{pops->masters_mm, n_mm, nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
+    StepArgs step{pops->states, pops->masters_mm, nullptr, pops->best_masters, n_mm, 0, 0,
+                  pops->history, pops->history_cap, 1, 1, pops->seeds, 2};
+    return rollout_impl(ticks, val_eps, params, src, false, H, val_fitness, val_trades, workspace, workspace_bytes,
+                        step, s);
+}
+
+extern "C" int sgmm_validate_multi(const sgmm_ticks* ticks, const sgmm_episodes* val_eps,
+                                   const sgmm_env_params* params, const sgmm_populations* pops,
+                                   double* val_fitness, int32_t* val_trades, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+    clear_error();
+    if (int rc = check_pops(pops)) return rc;
+    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes,
+                         as_stream(stream));
+}
+
+extern "C" int sgmm_generation_multi_best(const sgmm_ticks* ticks, const sgmm_episodes* train_eps,
+                                          const sgmm_episodes* val_eps, const sgmm_env_params* params,
+                                          const sgmm_populations* pops, double* fitness, int32_t* trades,
+                                          double* val_fitness, int32_t* val_trades, void* workspace,
+                                          size_t workspace_bytes, void* stream) {
+    clear_error();
+    if (int rc = check_pops(pops)) return rc;
+    const int32_t H = pops->hidden, K = pops->n_pop, P = pops->P;
+    if (int rc = check_episodes(ticks, train_eps, params, pops->masters_mm, H)) return rc;
+    SGMM_REQUIRE((int64_t)train_eps->n == (int64_t)K * P, "training episodes must be n_pop x P = %lld, got %d",
+                 (int64_t)K * P, train_eps->n);
+    SGMM_REQUIRE(val_eps && val_eps->n == K, "validation episodes must be one per population");
+    SGMM_REQUIRE(val_fitness && val_trades, "null validation outputs");
+    const int64_t n_mm = (int64_t)H * H + 7 * H + 2;
+    SGMM_REQUIRE(n_mm <= kMaxStepParams, "genome too large for the fused GA step");
+    const bool arl = pops->masters_adv != nullptr;
+    const int64_t n_adv = arl ? kAdvGenome : 0;
+    GenomeSrc src{nullptr, 0, nullptr, 0, pops->states, pops->masters_mm, pops->masters_adv, 0, 0};
+    src.pop_eps = P;
+    src.seeds = pops->seeds;
+    src.mm_pstride = n_mm;
+    src.adv_pstride = n_adv;
+    StepArgs step{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, n_mm, n_adv, 0,
+                  pops->history, pops->history_cap, P, P, pops->seeds, 1};
+    hipStream_t s = as_stream(stream);
+    if (int rc = rollout_impl(ticks, train_eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
+                              step, s))
+        return rc;
+    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s);
 }
 
 extern "C" int sgmm_rollout_fitness_asked_multi(const sgmm_ticks* ticks, const sgmm_episodes* eps,

@@ -329,8 +329,11 @@ class TrainingSession(_GraphedGenerations):
         n_loc = self.n_loc = self.i1 - self.i0
         n_cap = self.n_cap = shard_capacity(P, self.world)  # record slots per rank
         arl = self.arl = eng.use_arl
-        self.fused = eng.val_mode == "fused" or (eng.val_mode == "auto" and n_cap <= 512)
+        self.fused = not _best_validation(eng.val_mode, n_cap)
         self.torch_rng = eng.rng == "torch"
+        # device RNG, validation of the best: the populations path with K = 1
+        # (asked rollout + tell in its tail, then the new master's validation)
+        self.best_step = not self.torch_rng and not self.fused and G_ok(H)
         self.generations = int(generations)
         # (rng="torch" with world > 1: every rank draws the identical full
         # population from its identically seeded generator)
@@ -348,7 +351,7 @@ class TrainingSession(_GraphedGenerations):
 
         g_tr, o_tr, l_tr = phase(tr_off, self.T_tr)
         g_va, o_va, l_va = phase(va_off, self.T_va)
-        self.rec = FitnessRecords(P, self.world, dev, gather=self.sharded)
+        self.rec = FitnessRecords(P, self.world, dev, gather=self.sharded, with_val=not self.best_step)
         if self.fused:  # one launch: training + validation episodes of the shard
             adv = np.concatenate([g_tr, np.full(n_cap, -1)]) if arl else None  # validation: no adversary
             self.train_eps = EpisodeBatch(np.concatenate([g_tr, g_va]), np.concatenate([o_tr, o_va]),
@@ -368,7 +371,7 @@ class TrainingSession(_GraphedGenerations):
         # population rows: the full population when the host draws it (torch
         # RNG), else the shard's capacity (pads point at row 0, which exists)
         n_rows = P if self.torch_rng else max(n_cap, 1)
-        if not self.torch_rng and self.fused and G <= 4096:
+        if not self.torch_rng and G <= 4096:
             n_rows = 1  # asked population: generated inside the rollout (placeholder row)
         self.pop = torch.empty((n_rows, G), **f32)
         lo = min(self.i0, P - 1)
@@ -391,6 +394,10 @@ class TrainingSession(_GraphedGenerations):
         self.fast_step = (not self.torch_rng and self.fused and G <= 4096 and ADV_GENOME <= 4096)
         self.asked = AskedPopulation(self.state.data_ptr(), self.master.data_ptr(),
                                      self.master_adv.data_ptr() if arl else None, eng.seed, self.i0, 0)
+        self.seeds = torch.tensor([int(eng.seed)], dtype=torch.int64).to(dev)
+        self.pops = _lib.Populations(1, P, H, self.generations, self.state.data_ptr(), self.master.data_ptr(),
+                                     self.master_adv.data_ptr() if arl else None, self.best_master.data_ptr(),
+                                     self.seeds.data_ptr(), self.hist.data_ptr())
         # one generation = fixed launches -> replayable HIP graphs: the whole
         # generation on one rank; with several ranks the rollout and the boundary
         # are captured separately around the (eager) all-gather
@@ -424,6 +431,22 @@ class TrainingSession(_GraphedGenerations):
         including the GA step, is this one call."""
         P = self.P
         L, s = self.L, stream_ptr()
+        if self.best_step:
+            tk, ep = self.ticks.struct(), self.train_eps.struct()
+            ws = self.roll.workspace(self.train_eps, self.arl)
+            f, t = self.out
+            if not self.sharded:
+                vep = self.val_eps.struct()
+                vf, vt = self.vout
+                check(L.sgmm_generation_multi_best(ctypes.byref(tk), ctypes.byref(ep), ctypes.byref(vep),
+                                                   ptr(self.params), ctypes.byref(self.pops), ptr(f), ptr(t),
+                                                   ptr(vf), ptr(vt), ptr(ws), ws.numel(), s),
+                      "sgmm_generation_multi_best")
+            else:
+                check(L.sgmm_rollout_fitness_asked(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
+                                                   ctypes.byref(self.asked), self.H, ptr(f), ptr(t), ptr(ws),
+                                                   ws.numel(), s), "sgmm_rollout_fitness_asked")
+            return
         if self.fast_step:
             tk, ep = self.ticks.struct(), self.train_eps.struct()
             ws = self.roll.workspace(self.train_eps, self.arl)
@@ -460,6 +483,16 @@ class TrainingSession(_GraphedGenerations):
         e, L, s = self.e, self.L, stream_ptr()
         P, G = self.P, self.G
         arl = self.arl
+        if self.best_step:
+            if self.sharded:  # every rank: tell on the gathered records, then validate the new master
+                check(L.sgmm_ga_tell_multi(ctypes.byref(self.pops), *self.rec.tell_args(), s), "sgmm_ga_tell_multi")
+                tk, vep = self.ticks.struct(), self.val_eps.struct()
+                ws = self.roll.workspace(self.val_eps, False)
+                vf, vt = self.vout
+                check(L.sgmm_validate_multi(ctypes.byref(tk), ctypes.byref(vep), ptr(self.params),
+                                            ctypes.byref(self.pops), ptr(vf), ptr(vt), ptr(ws), ws.numel(), s),
+                      "sgmm_validate_multi")
+            return
         if self.fast_step:
             if self.sharded:
                 check(L.sgmm_ga_step(ptr(self.state), *self.rec.step_args(),
@@ -575,9 +608,9 @@ class MultiDRLEngine:
 
     @property
     def fused_path(self) -> bool:
-        """All populations on the one-launch device path (else: one after another)."""
-        return all(e.rng == "device" and e.val_mode in ("fused", "auto") and genome_size(e.hidden_dim) <= 4096
-                   for e in self.engines)
+        """All populations on the shared device path (else: one after another)."""
+        return all(e.rng == "device" and genome_size(e.hidden_dim) <= 4096 for e in self.engines) and \
+            len({e.val_mode for e in self.engines}) == 1
 
     def session(self, train_bundles, val_bundles, train_stats, generations=100, output_prefix="agent"):
         return MultiSession(self, train_bundles, val_bundles, train_stats, generations, output_prefix)
@@ -647,12 +680,19 @@ class MultiSession(_GraphedGenerations):
         self.T_tr = [s[0][1] for s in segs]
         self.params = params_tensor([EnvConfig(phi=e.phi, tick_size=e.tick_size, fee_rate=e.fee_rate)
                                      for e in engs], dev)
-        # episodes: per population n training slots then n validation slots
-        # (the shard's n_loc individuals first, zero-length pads after)
+        # validation: "fused" validates every individual inside the training
+        # launch (one launch pair per generation); "best" validates only each
+        # population's new master after the tell (the reference's order:
+        # sgmm_generation_multi_best, four launches but K validation episodes
+        # instead of K * P)
+        self.best_val = _best_validation(e0.val_mode, n, K)
+        # episodes: per population n training slots (then n validation slots
+        # when fused) -- the shard's n_loc individuals first, zero-length pads after
         pad = n - n_loc
         g, off, ln, par, adv = [], [], [], [], []
         for k, ((to, T), (vo, Tv)) in enumerate(segs):
-            for o, L_, is_tr in ((to, T, True), (vo, Tv, False)):
+            phases = ((to, T, True),) if self.best_val else ((to, T, True), (vo, Tv, False))
+            for o, L_, is_tr in phases:
                 g.append(np.concatenate([np.arange(n_loc), np.zeros(pad, np.int64)]))
                 off.append(np.full(n, o))
                 ln.append(np.concatenate([np.full(n_loc, L_), np.zeros(pad, np.int64)]))
@@ -660,7 +700,13 @@ class MultiSession(_GraphedGenerations):
                 adv.append(g[-1] if is_tr else np.full(n, -1))  # validation: no adversary
         self.eps = EpisodeBatch(np.concatenate(g), np.concatenate(off), np.concatenate(ln), np.concatenate(par),
                                 adv=np.concatenate(adv) if arl else None).to(dev)
-        self.rec = FitnessRecords(P, self.world, dev, n_pop=K, gather=self.sharded)
+        # best: one validation episode per population, genome row k = master k
+        self.val_eps = EpisodeBatch(np.arange(K), np.array([s[1][0] for s in segs]),
+                                    np.array([s[1][1] for s in segs]), np.arange(K)).to(dev) \
+            if self.best_val else None
+        self.vout = (torch.zeros(K, dtype=torch.float64, device=dev),
+                     torch.zeros(K, dtype=torch.int32, device=dev)) if self.best_val else None
+        self.rec = FitnessRecords(P, self.world, dev, n_pop=K, gather=self.sharded, with_val=not self.best_val)
         f32 = dict(dtype=torch.float32, device=dev)
         self.masters = torch.stack([e.mm_evolver.master_policy.get_weights() for e in engs]).to(**f32).contiguous()
         self.masters_adv = torch.stack([e.adv_evolver.master_policy.get_weights() for e in engs]).to(**f32) \
@@ -681,6 +727,8 @@ class MultiSession(_GraphedGenerations):
         self.graphs, self.batch_graph, self.full_graph = None, None, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, e0.sync_every))
         self.roll.reserve(self.eps, arl)
+        if self.val_eps is not None:
+            self.roll.reserve(self.val_eps, False)
         self.best_paths = [os.path.join(e.save_dir, f"{output_prefix}_best_val_{e.phi}.pth") for e in engs]
         self.saved_any = [False] * K
         self.emitted = 0
@@ -692,13 +740,21 @@ class MultiSession(_GraphedGenerations):
         tk, ep = self.ticks.struct(), self.eps.struct()
         ws = self.roll.workspace(self.eps, self.arl)
         f, t = self.rec.both
-        if not self.sharded:
+        if not self.sharded and self.best_val:
+            vep = self.val_eps.struct()
+            vf, vt = self.vout
+            check(self.L.sgmm_generation_multi_best(ctypes.byref(tk), ctypes.byref(ep), ctypes.byref(vep),
+                                                    ptr(self.params), ctypes.byref(self.pops), ptr(f), ptr(t),
+                                                    ptr(vf), ptr(vt), ptr(ws), ws.numel(), stream_ptr()),
+                  "sgmm_generation_multi_best")
+        elif not self.sharded:
             check(self.L.sgmm_generation_multi(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
                                                ctypes.byref(self.pops), ptr(f), ptr(t), ptr(ws), ws.numel(),
                                                stream_ptr()), "sgmm_generation_multi")
         else:
+            per_pop = self.n_cap if self.best_val else 2 * self.n_cap
             check(self.L.sgmm_rollout_fitness_asked_multi(ctypes.byref(tk), ctypes.byref(ep), ptr(self.params),
-                                                          ctypes.byref(self.pops), self.i0, 2 * self.n_cap,
+                                                          ctypes.byref(self.pops), self.i0, per_pop,
                                                           ptr(f), ptr(t), ptr(ws), ws.numel(), stream_ptr()),
                   "sgmm_rollout_fitness_asked_multi")
 
@@ -707,7 +763,18 @@ class MultiSession(_GraphedGenerations):
             self.rec.all_gather(self.group)
 
     def _boundary(self):
-        if self.sharded:
+        if not self.sharded:
+            return
+        if self.best_val:  # every rank: tell on the gathered records, then validate the new masters
+            check(self.L.sgmm_ga_tell_multi(ctypes.byref(self.pops), *self.rec.tell_args(), stream_ptr()),
+                  "sgmm_ga_tell_multi")
+            tk, vep = self.ticks.struct(), self.val_eps.struct()
+            ws = self.roll.workspace(self.val_eps, False)
+            vf, vt = self.vout
+            check(self.L.sgmm_validate_multi(ctypes.byref(tk), ctypes.byref(vep), ptr(self.params),
+                                             ctypes.byref(self.pops), ptr(vf), ptr(vt), ptr(ws), ws.numel(),
+                                             stream_ptr()), "sgmm_validate_multi")
+        else:
             check(self.L.sgmm_ga_step_multi(ctypes.byref(self.pops), *self.rec.multi_step_args(), stream_ptr()),
                   "sgmm_ga_step_multi")
 
@@ -762,6 +829,23 @@ class MultiSession(_GraphedGenerations):
 
 
 # ---------------------------------------------------------------------- small helpers
+# val_mode="auto": validate only the best (after the tell) from this many
+# individuals per population shard; below it the fused launch's extra
+# validation episodes cost less than the two extra launches
+BEST_VAL_MIN_SHARD = 256
+
+
+def G_ok(hidden: int) -> bool:
+    """Genomes small enough for the device GA step (and the adversary's)."""
+    return genome_size(hidden) <= 4096 and ADV_GENOME <= 4096
+
+
+def _best_validation(val_mode: str, n_shard: int, n_pop: int = 1) -> bool:
+    if val_mode not in ("auto", "fused", "best"):
+        raise ValueError("val_mode must be 'auto', 'fused' or 'best'")
+    return val_mode == "best" or (val_mode == "auto" and n_shard >= BEST_VAL_MIN_SHARD)
+
+
 def ctypes_size(t):
     import ctypes
     return ctypes.sizeof(t)

@@ -56,24 +56,31 @@ class FitnessRecords:
     With K populations (n_pop) the record holds every population's shard:
     f64 fitness[K][2n] then i32 trades[K][2n] (24 K n bytes); population k's
     fields sit at k * 16n (fitness) and 16Kn + k * 8n (trades) -- K = 1 is the
-    single-population layout above."""
+    single-population layout above.
 
-    def __init__(self, P: int, world: int, device, n_pop: int = 1, gather: bool | None = None):
+    with_val=False (validation of the best only, after the tell): training
+    results alone, f64 fitness[K][n] then i32 trades[K][n] (12 K n bytes)."""
+
+    def __init__(self, P: int, world: int, device, n_pop: int = 1, gather: bool | None = None,
+                 with_val: bool = True):
         # gather: keep a gathered buffer and exchange even at world 1 (the
         # sharded path rehearsed on one process); default: world > 1
         self.P, self.world, self.K = int(P), int(world), int(n_pop)
         self.sharded = bool(world > 1 if gather is None else gather)
+        self.with_val = bool(with_val)
         n = self.n = shard_capacity(P, world)
         K = self.K
         self.device = torch.device(device)
-        self.rec = torch.zeros(K * record_bytes(n), dtype=torch.uint8, device=self.device)
-        f = self.rec[:16 * K * n].view(torch.float64)
-        t = self.rec[16 * K * n:].view(torch.int32)
+        per = 2 if self.with_val else 1  # results per individual slot
+        self.rbytes = 12 * per * n  # one population's record
+        self.rec = torch.zeros(K * self.rbytes, dtype=torch.uint8, device=self.device)
+        f = self.rec[:8 * per * K * n].view(torch.float64)
+        t = self.rec[8 * per * K * n:].view(torch.int32)
         self.f, self.t = f, t
         self.train = (f[:n], t[:n])
-        self.val = (f[n:2 * n], t[n:2 * n])
+        self.val = (f[n:2 * n], t[n:2 * n]) if self.with_val else None
         self.both = (f, t)  # per population train then validation, for one fused launch
-        self.gathered = torch.zeros(world * K * record_bytes(n), dtype=torch.uint8, device=self.device) \
+        self.gathered = torch.zeros(world * K * self.rbytes, dtype=torch.uint8, device=self.device) \
             if self.sharded else None
         self._host = None
 
@@ -121,6 +128,18 @@ class FitnessRecords:
         ptrs = tuple(ctypes.c_void_p(base + o) for o in offs)
         shard = (n, K * record_bytes(n)) if self.sharded else (0, 0)
         return ptrs + (16 * n, 8 * n) + shard
+
+    def tell_args(self):
+        """(fit, trades, fit_pop_stride, trades_pop_stride, shard_n, shard_stride):
+        the arguments of sgmm_ga_tell_multi over the training results (either
+        layout), gathered or local."""
+        import ctypes
+        n, K = self.n, self.K
+        per = 2 if self.with_val else 1
+        base = (self.gathered if self.sharded else self.rec).data_ptr()
+        ptrs = (ctypes.c_void_p(base), ctypes.c_void_p(base + 8 * per * K * n))
+        shard = (n, K * self.rbytes) if self.sharded else (0, 0)
+        return ptrs + (8 * per * n, 4 * per * n) + shard
 
     def population(self):
         """Contiguous (train_f f64[P], train_t i32[P], val_f, val_t) of the whole

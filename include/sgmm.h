@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SGMM_ABI_VERSION 2
+#define SGMM_ABI_VERSION 3
 
 enum {
     SGMM_OK = 0,
@@ -324,6 +324,41 @@ int sgmm_rollout_fitness_asked_multi(const sgmm_ticks *ticks, const sgmm_episode
                                      int32_t i0, int32_t n_eps_pop, double *fitness,
                                      int32_t *trades, void *workspace, size_t workspace_bytes,
                                      void *stream);
+
+/* One generation of K populations in the reference's order
+ * (Env/drl_engine.py:92-171): the asked populations' training episodes
+ * (train_eps: population k owns [kP, (k+1)P), individual genome[e]), the
+ * tell of both evolvers in the training scan's tail (per population, its
+ * last workgroup), then ONE validation episode per population on its new
+ * master (sgmm_validate_multi) -- instead of validating every individual in
+ * the training launch (sgmm_generation_multi).  Four kernel launches;
+ * fitness/trades [K*P] (training), val_fitness/val_trades [K].  The workspace
+ * must hold the larger of the two batches (sgmm_rollout_workspace_size). */
+int sgmm_generation_multi_best(const sgmm_ticks *ticks, const sgmm_episodes *train_eps,
+                               const sgmm_episodes *val_eps, const sgmm_env_params *params,
+                               const sgmm_populations *pops, double *fitness, int32_t *trades,
+                               double *val_fitness, int32_t *val_trades, void *workspace,
+                               size_t workspace_bytes, void *stream);
+
+/* Validation of each population's current master (drl_engine.py:129-160),
+ * after a tell (sgmm_ga_tell_multi, or the tail of sgmm_generation_multi_best):
+ * val_eps holds one episode per population, episode k with genome[k] = k (row
+ * k of masters_mm) and no adversary.  Then per population: improvement test
+ * (strictly greater), checkpoint copy into best_masters, sigma decay, the
+ * history row's validation fields, gen + 1.  Two kernel launches. */
+int sgmm_validate_multi(const sgmm_ticks *ticks, const sgmm_episodes *val_eps,
+                        const sgmm_env_params *params, const sgmm_populations *pops,
+                        double *val_fitness, int32_t *val_trades, void *workspace,
+                        size_t workspace_bytes, void *stream);
+
+/* The tell of sgmm_ga_step_multi alone (NeuroEvolution.tell of both
+ * evolvers, model.py:73-76, drl_engine.py:119-125): argmax, masters
+ * regenerated, best index / training record into the state and history;
+ * sgmm_validate_multi completes the generation (multi-GPU: every rank runs
+ * both on the gathered training records). */
+int sgmm_ga_tell_multi(const sgmm_populations *pops, const double *fitness, const int32_t *trades,
+                       int64_t fit_pop_stride, int64_t trades_pop_stride, int32_t shard_n,
+                       int64_t shard_stride, void *stream);
 
 /* sgmm_ga_step for each of the K populations (one workgroup each, one
  * launch): population k reads its records at byte offset k * fit_pop_stride

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(sgmm):
     assert declared <= exported, declared - exported
     assert exported <= declared, exported - declared  # nothing undocumented
     assert set(_lib.SIGNATURES) == declared            # the binding covers the header
-    assert L.sgmm_abi_version() == 2
+    assert L.sgmm_abi_version() == 3
 
 
 def test_struct_layouts_match_header(sgmm):

@@ -28,12 +28,12 @@ def _bundles():
 POPS = [(0.0001, 0.001, 0), (0.005, 0.001, 0), (0.01, 0.01, 1)]
 
 
-def _engine(sgmm, k, P, arl, save_dir, H=16):
+def _engine(sgmm, k, P, arl, save_dir, H=16, val_mode="fused", use_graph=True):
     phi, tick, _ = POPS[k]
     torch.manual_seed(100 + k)  # the initial master (and adversary master) come from the torch generator
     return sgmm.DRLEngine(pop_size=P, phi=phi, tick_size=tick, use_arl=arl, save_dir=save_dir, hidden_dim=H,
-                          rng="device", seed=1000 + 7 * k, val_mode="fused", sync_every=5, patience=3,
-                          verbose=False)
+                          rng="device", seed=1000 + 7 * k, val_mode=val_mode, sync_every=5, patience=3,
+                          verbose=False, use_graph=use_graph)
 
 
 @pytest.mark.parametrize("P,arl", [(24, False), (24, True), (300, False), (600, False)])
@@ -85,3 +85,47 @@ def test_multi_sweep_constructor_and_shared_bundle(sgmm, tmp_path):
         pol, hist = e.train(tr, va, st, generations=8)
         assert np.array_equal(np.array(res[k][1]["train_f"]), np.array(hist["train_f"])), phi
         assert np.array_equal(res[k][0].get_weights().numpy(), pol.get_weights().numpy()), phi
+
+
+@pytest.mark.parametrize("P,arl,use_graph", [(24, False, True), (24, True, True), (300, False, False),
+                                             (300, True, True)])
+def test_best_validation_equals_fused(sgmm, tmp_path, P, arl, use_graph):
+    """val_mode="best" (sgmm_generation_multi_best: training launch with the
+    tell in its tail, then ONE validation episode per population on the new
+    master, drl_engine.py:127-138) == val_mode="fused" (every individual
+    validated inside the training launch, the best's record picked): the
+    validation of the best is the same episode on the same genome, so the
+    histories, masters, sigma schedules and checkpoints agree bit for bit."""
+    assets = _bundles()
+    gens = 12
+    tr = [assets[a][0] for _, _, a in POPS]
+    va = [assets[a][1] for _, _, a in POPS]
+    st = [assets[a][2] for _, _, a in POPS]
+    out = {}
+    for vm in ("fused", "best"):
+        m = sgmm.MultiDRLEngine([_engine(sgmm, k, P, arl, str(tmp_path / vm), val_mode=vm, use_graph=use_graph)
+                                 for k in range(len(POPS))])
+        sess = m.session(tr, va, st, generations=gens)
+        assert sess.best_val == (vm == "best")
+        for g0 in range(0, gens, 5):
+            n = min(5, gens - g0)
+            sess.steps(g0, n)
+            if n == 5:
+                sess.flush(g0 + n)
+        out[vm] = (sess.finish(), m)
+    (rf, mf), (rb, mb) = out["fused"], out["best"]
+    for k in range(len(POPS)):
+        (pf, hf), (pb, hb) = rf[k], rb[k]
+        for key in hf:
+            assert np.array_equal(np.array(hf[key], np.float64), np.array(hb[key], np.float64), equal_nan=True), \
+                (k, key)
+        assert np.array_equal(pf.get_weights().numpy(), pb.get_weights().numpy()), k
+        assert mf.engines[k].mm_evolver.sigma == mb.engines[k].mm_evolver.sigma, k
+        if arl:
+            assert torch.equal(mf.engines[k].adv_evolver.master_policy.get_weights(),
+                               mb.engines[k].adv_evolver.master_policy.get_weights()), k
+        name = f"agent_best_val_{POPS[k][0]}.pth"
+        a = torch.load(os.path.join(tmp_path / "fused", name), weights_only=True)
+        b = torch.load(os.path.join(tmp_path / "best", name), weights_only=True)
+        assert all(torch.equal(a[x], b[x]) for x in b), k
+    assert any(f < 0.05 for f in (e.mm_evolver.sigma for e in mb.engines))  # patience 3: a decay happened

@@ -50,22 +50,27 @@ def _bundles():
     return tr, va, synthetic.train_stats(tr)
 
 
-def _multi(sgmm, tmp, exchange, arl=False):
+def _multi(sgmm, tmp, exchange, arl=False, val_mode="fused"):
     engines = []
     for k, phi in enumerate((0.0001, 0.005)):
         torch.manual_seed(300 + k)
         engines.append(sgmm.DRLEngine(pop_size=40, phi=phi, tick_size=0.001, use_arl=arl, save_dir=str(tmp),
-                                      hidden_dim=16, rng="device", seed=77 + k, val_mode="fused", sync_every=8,
+                                      hidden_dim=16, rng="device", seed=77 + k, val_mode=val_mode, sync_every=8,
                                       patience=3, verbose=False, exchange=exchange))
     return sgmm.MultiDRLEngine(engines)
 
 
-@pytest.mark.parametrize("arl", [False, True], ids=["mm", "arl"])
-def test_rccl_exchange_in_graph_equals_single_process(sgmm, tmp_path, nccl_world1, arl):
+@pytest.mark.parametrize("arl,val_mode", [(False, "fused"), (True, "fused"), (False, "best"), (True, "best")],
+                         ids=["mm", "arl", "mm-best", "arl-best"])
+def test_rccl_exchange_in_graph_equals_single_process(sgmm, tmp_path, nccl_world1, arl, val_mode):
+    """best: the ranks gather training records only, then every rank runs the
+    tell (sgmm_ga_tell_multi) and validates the new masters
+    (sgmm_validate_multi), all inside the captured graphs; the reference
+    result is the one-process fused training."""
     tr, va, st = _bundles()
     gens = 20  # one 8-generation batch graph twice, then 4 single-generation replays
     ref = _multi(sgmm, tmp_path / "ref", "auto", arl).train(tr, va, st, generations=gens)
-    m = _multi(sgmm, tmp_path / "rccl", "always", arl)
+    m = _multi(sgmm, tmp_path / "rccl", "always", arl, val_mode)
     sess = m.session(tr, va, st, generations=gens)
     assert sess.sharded and sess.world == 1
     for g0 in range(0, gens, 8):
@@ -86,17 +91,22 @@ def test_rccl_single_population_session(sgmm, tmp_path, nccl_world1):
     """DRLEngine (one population) on the same forced-exchange path."""
     tr, va, st = _bundles()
     out = {}
-    for ex in ("auto", "always"):
+    for ex, vm in (("auto", "fused"), ("always", "fused"), ("always", "best"), ("auto", "best")):
         torch.manual_seed(5)
-        e = sgmm.DRLEngine(pop_size=48, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / ex), hidden_dim=32,
-                           rng="device", seed=9, sync_every=8, verbose=False, exchange=ex)
+        e = sgmm.DRLEngine(pop_size=48, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / (ex + vm)),
+                           hidden_dim=32, rng="device", seed=9, sync_every=8, verbose=False, exchange=ex,
+                           val_mode=vm, patience=3)
         sess = e.session(tr, va, st, generations=16)
         sess.steps(0, 16)
         if ex == "always":
             assert sess.full_graph, getattr(sess, "capture_error", "")
+        assert sess.best_step == (vm == "best")
         pol, hist = sess.finish()
-        out[ex] = (pol.get_weights().numpy(), hist, e.mm_evolver.sigma)
-    (wa, ha, sa), (wb, hb, sb) = out["auto"], out["always"]
-    for key in ha:
-        assert np.array_equal(np.array(ha[key], np.float64), np.array(hb[key], np.float64), equal_nan=True), key
-    assert np.array_equal(wa, wb) and sa == sb
+        out[ex + vm] = (pol.get_weights().numpy(), hist, e.mm_evolver.sigma)
+    wa, ha, sa = out["autofused"]
+    for k2 in ("alwaysfused", "alwaysbest", "autobest"):
+        wb, hb, sb = out[k2]
+        for key in ha:
+            assert np.array_equal(np.array(ha[key], np.float64), np.array(hb[key], np.float64), equal_nan=True), \
+                (k2, key)
+        assert np.array_equal(wa, wb) and sa == sb, k2

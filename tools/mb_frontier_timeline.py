@@ -28,10 +28,11 @@ ticks = sg.TickStore(); s0 = ticks.add(tr, st); s1 = ticks.add(va, st); ticks.to
 params = sg.params_tensor([sg.EnvConfig(phi=1e-3, tick_size=0.001)], dev)
 pop = synthetic.population(K * P, H, sigma=0.05, seed=1).to(dev)
 gen, offs, lens = [], [], []
+VAL = not os.environ.get("TRAIN_ONLY")  # TRAIN_ONLY=1: the best-validation training launch
 for k in range(K):
-    gen += list(range(k * P, (k + 1) * P)) * 2
-    offs += [ticks.segments[s0][0]] * P + [ticks.segments[s1][0]] * P
-    lens += [4560] * P + [912] * P
+    gen += list(range(k * P, (k + 1) * P)) * (2 if VAL else 1)
+    offs += [ticks.segments[s0][0]] * P + ([ticks.segments[s1][0]] * P if VAL else [])
+    lens += [4560] * P + ([912] * P if VAL else [])
 n = len(gen)
 eb = sg.EpisodeBatch(np.array(gen), offs, lens, np.zeros(n)).to(dev)
 eng = sg.RolloutEngine(dev)
@@ -65,3 +66,16 @@ print(f"  waves per SIMD: mean {cnt.mean():.2f} max {cnt.max()}; per-SIMD sum of
 grid = np.linspace(0, e_.max(), 40)
 act = [(np.sum((s <= t) & (e_ > t))) for t in grid]
 print("  resident waves over time (/1024 SIMDs):", [round(a / 1024, 2) for a in act[::4]])
+# per-SIMD wave count vs when the SIMD finishes
+for c in np.unique(cnt):
+    m = cnt == c
+    print(f"  SIMDs with {c} waves: {m.sum():4d}; last end med {np.median(last[m]) / 1e3:.1f} us "
+          f"max {last[m].max() / 1e3:.1f}; wave duration med {np.median(dur[np.isin(inv, np.where(m)[0])]) / 1e3:.1f} us")
+cu_id = sid // 4
+uc, cinv = np.unique(cu_id, return_inverse=True)
+ccnt = np.bincount(cinv)
+print("  waves per CU: " + " ".join(f"{c}:{(ccnt == c).sum()}" for c in np.unique(ccnt)))
+xc = np.bincount(xcc, minlength=8)
+print("  waves per XCD:", list(xc))
+r = np.corrcoef(h[:, 2].astype(float), dur)[0, 1]
+print(f"  corr(slots, duration) {r:.2f}")
