@@ -53,6 +53,11 @@ struct EpArrays {
     const int32_t* param;
     int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
     const int32_t* order;  // frontier kernel: episode of workgroup b (NULL: b)
+    // frontier kernel: the episodes at order positions >= fwhole are split
+    // into two waves (two 64-chunk groups), the others run as one wave; the
+    // policy kernel records each episode's wave count in fnw[e] for the scan
+    int32_t fwhole;
+    uint32_t* fnw;
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -878,16 +883,21 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
 // the other chunks track every state in [inv_min, inv_max].  Arithmetic per
 // (tick, state) is the table's (same MFMA chains, same fp64 step), so every
 // output bit is the table's.
-constexpr int kFrontierSlots = 64;   // chunks (lanes) per episode
+constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
+constexpr int kFrontierMaxWaves = 2;   // waves (64-chunk groups) per episode
+constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunk slots per episode
 typedef __attribute__((address_space(3))) const float lds_cf;
 typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
-__host__ __device__ __forceinline__ int frontier_len(int T) {
-    const int c = (T + kFrontierSlots - 1) / kFrontierSlots;
+// ticks per chunk with nw waves (64 nw chunks) per episode
+__host__ __device__ __forceinline__ int frontier_len(int T, int nw) {
+    const int c = (T + kFrontierLanes * nw - 1) / (kFrontierLanes * nw);
     return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
 }
-// the episode's block of plane rows: frontier_len(T) x 64 <= T + 256 slots
-// (T rounded up to 64 chunks of a multiple of 4), so blocks at step_off + 256 e
-// never overlap; the plane stride covers total_steps + 256 n (rew_stride)
+// the episode's block of plane rows: nw groups of frontier_len(T, nw) x 64 rows
+// <= T + 256 nw slots (T rounded up to 64 nw chunks of a multiple of 4), so
+// blocks at step_off + 512 e never overlap; the plane stride covers
+// total_steps + 512 n (rew_stride).  Group g's row of tick offset u, lane l:
+// base + g * CL * 64 + u * 64 + l (tick-offset-major within the group)
 __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
     return step_off + (int64_t)4 * kFrontierSlots * e;
 }
@@ -901,14 +911,23 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16, KS = H / 4;
     constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
-    const int e = ep.order ? ep.order[blockIdx.x] : (int)blockIdx.x;  // longest episodes first
+    // wave b: the whole episode at order position b (b < fwhole), else chunk
+    // group g of a split episode (two waves each, longest episodes first)
+    const int b = (int)blockIdx.x;
+    const int pos = b < ep.fwhole ? b : ep.fwhole + ((b - ep.fwhole) >> 1);
+    const int nw = b < ep.fwhole ? 1 : 2, cg = b < ep.fwhole ? 0 : (b - ep.fwhole) & 1;
+    const int e = ep.order ? ep.order[pos] : pos;
+    if (cg == 0 && threadIdx.x == 0) ep.fnw[e] = (uint32_t)nw;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
-    const int CL = frontier_len(T);
+    const int CL = frontier_len(T, nw);
     const int nch = (T + CL - 1) / CL;
+    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
     const int lane = threadIdx.x, grp = lane >> 4, col = lane & 15;
+    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int t0 = lane * CL;                          // this lane's chunk
+    const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int t0 = c * CL;
     const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
 
     // LDS (~9 KB per wave, so 3 waves per SIMD fit): the genome is staged in
@@ -946,7 +965,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // per-lane path bookkeeping: byte s of cur = the state of the path that
     // started the chunk in state s (tracked starts: bits of sset)
     const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = lane >= nch ? 0u : (lane == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
     const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
     uint64_t cur = kIdentityMap;
     uint32_t cnt[NSI];
@@ -962,8 +981,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
 #endif
 #ifdef SGMM_STAMPS_PHASE
-    // per wave (episode): 0 cycles, 1 tile-slots, 2 slots, 3 layer 1-3 cycles,
-    // 4 FPT-step cycles, 5 per-tick head (frontier, signals, layer-1 terms), 6 planes
+    // per wave (episode): 0 cycles, 1 layers 1-2 (MFMA issue), 2 relu + transpose
+    // (MFMA drain), 3 layer 3, 4 FPT step, 5 per-tick head (frontier, signals,
+    // layer-1 terms), 6 planes, 7 wall time (10 ns ticks)
     unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
 #define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
@@ -991,11 +1011,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
         if (!act) fmask = 0;
         // slots per 16-lane tile: the most frontier states of any of its lanes
+        // (a row maximum in four DPP steps -- pairs, quads, half rows, rows --
+        // instead of four dependent LDS permutes)
         int ns = __builtin_popcount(fmask);
-        ns = max(ns, __shfl_xor(ns, 1, kWave));
-        ns = max(ns, __shfl_xor(ns, 2, kWave));
-        ns = max(ns, __shfl_xor(ns, 4, kWave));
-        ns = max(ns, __shfl_xor(ns, 8, kWave));
+        ns = max(ns, (int)dpp32<0xB1>(0u, (uint32_t)ns));   // quad_perm [1,0,3,2]
+        ns = max(ns, (int)dpp32<0x4E>(0u, (uint32_t)ns));   // quad_perm [2,3,0,1]
+        ns = max(ns, (int)dpp32<0x141>(0u, (uint32_t)ns));  // row_half_mirror
+        ns = max(ns, (int)dpp32<0x140>(0u, (uint32_t)ns));  // row_mirror
         int tsl[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) tsl[q] = __builtin_amdgcn_readlane(ns, 16 * q);
@@ -1010,6 +1032,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         asm volatile("" : "+v"(l1p));
         // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
         float pre[4][KS];
+        // the frontier of each B-operand sample's chunk (lane 16q + col): the
+        // slots take their k-th state from it, no per-slot permute
+        uint32_t remq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) remq[q] = (uint32_t)__shfl((int)fmask, 16 * q + col, kWave);
         {
             float xs0[4], xs1[4];
 #pragma unroll
@@ -1028,8 +1055,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         SGMM_FT(fs_b);
         fs_c[5] += fs_b - fs_a;
-        fs_c[2] += nslot;
-        fs_c[1] += (unsigned long long)(tsl[0] + tsl[1] + tsl[2] + tsl[3]);
 #endif
         uint32_t rem = fmask;
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
@@ -1045,7 +1070,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             const bool has = rem != 0u;
             const uint32_t f = has ? (uint32_t)__builtin_ctz(rem) : 0u;
             rem &= rem - 1u;
-            const float x2own = (float)((double)(inv_min + (int)f) / 2.0);
             // layer 1 + layer 2 for all four 16-lane tiles and both 16-neuron
             // halves: 4 x NT independent accumulator chains issued k-step by
             // k-step keep the matrix pipe busy (a tile-by-tile schedule waits
@@ -1053,9 +1077,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             // compute and discard (they are the exception: 5.2 of 5.4 tile-slots run)
             f32x4 acc[4][NT];
             {
+                // inv / 2 of sample 16q + col's k-th state (exact in float: |inv| <= 8)
                 float x2q[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) x2q[q] = __shfl(x2own, 16 * q + col, kWave);
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
+                    remq[q] &= remq[q] - 1u;
+                    x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
+                }
 #pragma unroll
                 for (int rt = 0; rt < NT; ++rt) {
                     const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
@@ -1076,6 +1105,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
                         }
                 }
             }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                SGMM_FT(t_);  // MFMAs issued (not completed)
+                fs_c[1] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1085,6 +1122,15 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
                     for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
                     *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
                 }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[2] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
             // layer 3 of this lane's sample, in neuron order (the canonical chain)
             float o0 = w3p[2 * H], o1 = w3p[2 * H + 1];
 #pragma unroll 1
@@ -1140,7 +1186,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             // the 64 chunks' rewards at offset u): one coalesced 512-byte store
             // per plane and tick; row-major rows made every 8-byte store a
             // partial line and the L2 wrote ~6x the bytes back
-            const int64_t row = frontier_base(so, e) + (int64_t)tt * kFrontierSlots + lane;
+            const int64_t row = rbase + (int64_t)tt * kFrontierLanes + lane;
 #pragma unroll
             for (int s = 0; s < NSI; ++s) {
                 if (!((sset >> s) & 1u)) continue;
@@ -1199,13 +1245,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         }
     }
 #endif
-    if (lane < nch) {
+    if (c < nch) {
         // untracked start states keep the identity byte (never on the episode's path)
         uint64_t cm = kIdentityMap;
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = (int64_t)e * kFrontierSlots + lane;
+        const int64_t ci = (int64_t)e * kFrontierSlots + c;
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = cnt[s];
@@ -1656,7 +1702,7 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     __shared__ int red_trades;
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
-    const int CL = FR ? frontier_len(T) : kChunk;
+    const int CL = FR ? frontier_len(T, (int)ep.fnw[e]) : kChunk;
     const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
     const int64_t cb = FR ? (int64_t)e * kFrontierSlots : (int64_t)chunk_base(so, e);
@@ -1703,11 +1749,12 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
                 const uint32_t ki = kin[c];
                 const int kc = (int)(ki & 0x1FFFFFFFu);
                 const int64_t pst = start[c], pp0 = ki >> 29;
-                const int64_t rb = frontier_base(so, e) + c;
+                const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
+                                   c % kFrontierLanes;
 #pragma unroll
                 for (int j = 0; j < kSumTpt; ++j) {
                     const int jj = min(j, n - 1 - i0);
-                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierSlots];
+                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
                 }
             } else {
                 const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
@@ -2033,12 +2080,12 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     return SGMM_OK;
 }
 
-// plane stride: every tick plus the frontier layout's 256 padding slots per episode
-static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + 256 * n + 31) & ~int64_t(31); }
+// plane stride: every tick plus the frontier layout's 512 padding slots per episode
+static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + 4 * kFrontierSlots * n + 31) & ~int64_t(31); }
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps, e->n), e->order};
+                    e->param, rew_stride(e->total_steps, e->n), e->order, e->n, nullptr};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -2079,7 +2126,8 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 //                 rounded up to 32)
 //   adversary:    u64 fills[total_steps] | f64 rew[total_steps][n_states]
 //   (frontier kernel: cmaps / ctr hold u64 maps / u32[8] trade counts at slots
-//   e * 64 + c, then u32 kinfo[n * 64]; the sections are sized for both)
+//   e * 128 + c, then u32 kinfo[n * 128] and u32 waves[n] -- each episode's
+//   wave count; the sections are sized for both)
 static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
 static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierSlots; }
 static size_t ws_cmaps(int32_t n, int64_t steps) {
@@ -2088,7 +2136,7 @@ static size_t ws_cmaps(int32_t n, int64_t steps) {
 static size_t ws_ctr(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps) * sizeof(uint64_t), n_frontier_slots(n) * 8 * sizeof(uint32_t)));
 }
-static size_t ws_kinfo(int32_t n) { return align256(n_frontier_slots(n) * sizeof(uint32_t)); }
+static size_t ws_kinfo(int32_t n) { return align256((n_frontier_slots(n) + n) * sizeof(uint32_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
@@ -2113,6 +2161,34 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     if (v && std::strcmp(v, "frontier") == 0) return true;
     if (v && *v) return false;
     return eps->n >= kFrontierMinEps;
+}
+
+// How many episodes run as one wave in the frontier kernel (the longest
+// fwhole of the order); the rest are split into two waves (two 64-chunk
+// groups of half the length, at the cost of more start-state paths to
+// merge).  A whole episode is a long serial walk and every SIMD holds three
+// waves (occupancy), so the split count evens the load: 3 x SIMDs units, e.g.
+// 2560 episodes on 1024 SIMDs -> 2048 whole + 512 split = 3072 waves, two
+// whole and one half episode per SIMD instead of 512 SIMDs with three whole
+// episodes.  SGMM_FRONTIER_NW=1|2 forces all whole / all split.
+static int simd_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        n = 4 * cus;
+    }
+    return n;
+}
+static int32_t frontier_whole(int32_t n) {
+    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
+        if (std::atoi(v) == 1) return n;
+        if (std::atoi(v) == 2) return 0;
+    }
+    const int64_t split = std::min<int64_t>(n, std::max<int64_t>(0, 3LL * simd_count() - n));
+    return (int32_t)(n - split);
 }
 
 template <int H>
@@ -2243,14 +2319,18 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         kinfo = reinterpret_cast<uint32_t*>(w + a + b);
         rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n));
     }
-    const EpArrays ep = ep_arrays(eps, arl);
+    EpArrays ep = ep_arrays(eps, arl);
     const bool fr = use_frontier(arl, hidden, eps);
+    if (fr) {
+        ep.fwhole = frontier_whole(eps->n);
+        ep.fnw = kinfo + n_frontier_slots(eps->n);
+    }
     const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
     if (fr && eps->max_len > 0) {
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
-        const dim3 grid(eps->n), block(kWave);
+        const dim3 grid(ep.fwhole + 2 * (eps->n - ep.fwhole)), block(kWave);
 #define SGMM_FRONTIER(H_, NSI_)                                                                            \
     SGMM_LAUNCH((k_policy_frontier<H_, NSI_>), grid, block, 0, s, *ticks, ep, params, src, eps->inv_min, nsi, \
                 cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew)

@@ -60,9 +60,11 @@ def test_argument_errors_need_no_gpu(sgmm):
     assert rc == -1 and b"hidden" in L.sgmm_last_error()
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
-    # frontier kernel (64 chunk slots per episode: u64 map, u32[8] counts, u32 merge info)
-    # (planes: 1000 ticks + 256 padding slots per episode of the frontier layout, rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == 4 * 64 * 8 + 4 * 64 * 32 + 4 * 64 * 4 + 5 * 2048 * 8
+    # frontier kernel (128 chunk slots per episode: u64 map, u32[8] counts, u32 merge info;
+    # u32 wave count per episode) (planes: 1000 ticks + 512 padding slots per episode of the
+    # frontier layout, rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 128 * 8 + 4 * 128 * 32 + 2304
+                                                         + 5 * 3072 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)
@@ -72,8 +74,8 @@ def test_argument_errors_need_no_gpu(sgmm):
                             ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
     assert rc == -1 and b"bars per day" in L.sgmm_last_error()
     # adversary (20 states): u64 fill words + 64-byte chunk transducers (1000/64 + 4 + 1 slots)
-    # + per-state f64 reward planes (stride 1000 + 256 * 4 rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 2048 * 8
+    # + per-state f64 reward planes (stride 1000 + 512 * 4 rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 3072 * 8
 
 
 def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):

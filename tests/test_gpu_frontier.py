@@ -17,9 +17,12 @@ pytestmark = [pytest.mark.gpu,
 DEV = torch.device("cuda:0")
 
 
-@pytest.fixture
-def frontier(monkeypatch):
+@pytest.fixture(params=[1, 2], ids=["1wave", "2waves"])
+def frontier(monkeypatch, request):
+    """The frontier kernel with one wave (64 chunks) or two waves (128 chunks,
+    two independent 64-chunk groups) per episode."""
     monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
+    monkeypatch.setenv("SGMM_FRONTIER_NW", str(request.param))
 
 
 def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
@@ -77,9 +80,12 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
     assert np.array_equal(fit, wf)
 
 
-def test_frontier_default_selection_many_episodes(sgmm, oracle):
+@pytest.mark.parametrize("nw", ["", "1", "2"], ids=["default", "1wave", "2waves"])
+def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
     """From 2048 episodes on the frontier kernel is the default: 2100 ragged
     episodes bit-exact against the oracle."""
+    if nw:
+        monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
     lens = 300 + (np.arange(2100) * 37) % 900
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=47, sigma=0.3)
     assert np.array_equal(trd, wt)

@@ -1,8 +1,8 @@
 """Diagnostic: per-wave phase cycles of the frontier kernel (stamped library,
 tools/build_stamps.sh), on a config-3-shaped batch: P individuals x (one
 4560-tick training episode + one 912-tick validation episode), H=32.
-Per wave: 0 cycles, 1 tile-slots (16-lane MFMA tiles run), 2 slots (frontier
-passes), 3 layer 1-3 cycles, 4 FPT-step cycles, 5 per-tick head, 6 planes."""
+Per wave: cycles in layers 1-2 (MFMA issue), relu + transpose (MFMA drain),
+layer 3, the FPT step, the per-tick head and the plane writes."""
 import ctypes
 import os
 import sys
@@ -47,7 +47,7 @@ for name, sl, T in (("train", slice(0, P), 4560), ("val", slice(P, P + NV), 912)
     print(f"{name}: T={T} chunk={CL} waves={len(x)}")
     print(f"  cycles/wave {med(x[:, 0]):9.0f}   per tick {med(x[:, 0]) / CL:7.0f}   wall {med(x[:, 7]) / 100:8.1f} us"
           f"   shader clock {med(x[:, 0] / np.maximum(x[:, 7], 1)) / 10:6.3f} GHz")
-    print(f"  slots/tick {med(x[:, 2]) / CL:5.2f}   tile-slots/tick {med(x[:, 1]) / CL:5.2f}")
-    for k, lab in ((3, "layer 1-3"), (4, "FPT step"), (5, "tick head"), (6, "planes")):
+    for k, lab in ((1, "layer 1-2"), (2, "transpose"), (3, "layer 3"), (4, "FPT step"), (5, "tick head"),
+                   (6, "planes")):
         print(f"  {lab:10s} {med(x[:, k]):9.0f} cyc/wave = {med(x[:, k]) / med(x[:, 0]) * 100:5.1f} %"
-              f"   per slot {med(x[:, k]) / max(1, med(x[:, 2])):6.0f}   per tile-slot {med(x[:, k]) / max(1, med(x[:, 1])):6.0f}")
+              f"   per tick {med(x[:, k]) / CL:6.0f}")

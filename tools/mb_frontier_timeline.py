@@ -52,6 +52,8 @@ sid = ((xcc * 8 + se) * 16 + cu) * 4 + simd
 lens = np.array(lens)
 print(f"waves {n}; kernel span {e_.max() / 1e3:.1f} us; distinct SIMDs {len(np.unique(sid))}")
 for name, m in (("train", lens == 4560), ("val", lens == 912)):
+    if not m.any():
+        continue
     print(f"  {name}: duration med {np.median(dur[m]) / 1e3:.1f} us p10 {np.percentile(dur[m], 10) / 1e3:.1f} "
           f"p90 {np.percentile(dur[m], 90) / 1e3:.1f}; start med {np.median(s[m]) / 1e3:.1f} us "
           f"max {s[m].max() / 1e3:.1f}; slots/wave {np.median(h[m, 2]):.0f} tile-slots {np.median(h[m, 3]):.0f}")
@@ -79,3 +81,11 @@ xc = np.bincount(xcc, minlength=8)
 print("  waves per XCD:", list(xc))
 r = np.corrcoef(h[:, 2].astype(float), dur)[0, 1]
 print(f"  corr(slots, duration) {r:.2f}")
+sl = h[:, 2].astype(float)
+print("  slots/wave percentiles 50/90/99/max:", [float(np.percentile(sl, p)) for p in (50, 90, 99)], float(sl.max()))
+top = np.argsort(-e_)[:12]
+print("  last-ending waves: (end us, dur us, slots, waves on its SIMD)")
+for w in top:
+    print(f"    {e_[w] / 1e3:7.1f} {dur[w] / 1e3:7.1f} {int(sl[w]):5d} {cnt[inv[w]]}")
+hs = np.argsort(-sl)[:8]
+print("  heaviest waves: (slots, dur us, end us, waves on SIMD)", [(int(sl[w]), round(dur[w] / 1e3, 1), round(e_[w] / 1e3, 1), int(cnt[inv[w]])) for w in hs])
