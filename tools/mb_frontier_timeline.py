@@ -89,3 +89,13 @@ for w in top:
     print(f"    {e_[w] / 1e3:7.1f} {dur[w] / 1e3:7.1f} {int(sl[w]):5d} {cnt[inv[w]]}")
 hs = np.argsort(-sl)[:8]
 print("  heaviest waves: (slots, dur us, end us, waves on SIMD)", [(int(sl[w]), round(dur[w] / 1e3, 1), round(e_[w] / 1e3, 1), int(cnt[inv[w]])) for w in hs])
+# is a SIMD's end set by the matrix work on it?  per-SIMD slot total vs its last end
+simd_slots = np.bincount(inv, weights=sl)
+A = np.vstack([simd_slots, np.ones_like(simd_slots)]).T
+coef, *_ = np.linalg.lstsq(A, last / 1e3, rcond=None)
+print(f"  per-SIMD slots: mean {simd_slots.mean():.0f} max {simd_slots.max():.0f}; last end ~ {coef[0]:.3f} us/slot "
+      f"+ {coef[1]:.1f} us, corr {np.corrcoef(simd_slots, last)[0, 1]:.2f}")
+for lo, hi in ((0, 200), (200, 260), (260, 320), (320, 400), (400, 2000)):
+    m = (simd_slots >= lo) & (simd_slots < hi)
+    if m.any():
+        print(f"    SIMDs with {lo}-{hi} slots: {m.sum():4d}, last end med {np.median(last[m]) / 1e3:.1f} max {last[m].max() / 1e3:.1f} us")
