@@ -1559,7 +1559,7 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
             L.S = ib ? from_binade(M, e) : S;
         }
 #ifdef SGMM_STAMPS
-        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] = n_iter; g_stamps[blockIdx.x][14] = n_slow; }
+        if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] += n_iter; g_stamps[blockIdx.x][14] += n_slow; }
 #endif
         if (lane == 0 && nblk == 0) L.S = S;
     }
@@ -1736,40 +1736,80 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     }
     __syncthreads();
     SGMM_STAMP(e, 1);
+#ifdef SGMM_STAMPS
+    // per episode, summed over the windows: 11 gather cycles, 12 sum cycles,
+    // 15 windows; 13 / 14 walk iterations / fallback blocks
+    unsigned long long sw_a, sw_b, sw_g = 0, sw_s = 0, sw_n = 0;
+    if (tid == 0 && e < 4096) g_stamps[e][13] = g_stamps[e][14] = 0;
+#define SGMM_SW(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+#endif
     double S = 0.0;  // exact running sum (identical in every thread between windows)
-    for (int w0 = 0; w0 < T; w0 += kWin) {
+    // a window's rewards: each thread's NT / TPB groups of kSumTpt ticks (4
+    // ticks of one chunk, CL % kSumTpt == 0) gathered into registers; the next
+    // window's loads are issued before this window's exact sum, so their
+    // latency hides behind the sum's serial walk
+    double r[NT / TPB][kSumTpt];
+    auto gather = [&](int w0) {
         const int n = min(kWin, T - w0);
 #pragma unroll
         for (int g = 0; g < NT / TPB; ++g) {
-        const int i0 = (g * TPB + tid) * kSumTpt;
-        if (i0 < n) {  // 4 ticks of one chunk (CL % kSumTpt == 0)
-            double r[kSumTpt];
-            if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
-                const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
-                const uint32_t ki = kin[c];
-                const int kc = (int)(ki & 0x1FFFFFFFu);
-                const int64_t pst = start[c], pp0 = ki >> 29;
-                const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
-                                   c % kFrontierLanes;
+            const int i0 = (g * TPB + tid) * kSumTpt;
+            if (i0 < n) {
+                if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
+                    const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
+                    const uint32_t ki = kin[c];
+                    const int kc = (int)(ki & 0x1FFFFFFFu);
+                    const int64_t pst = start[c], pp0 = ki >> 29;
+                    const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
+                                       c % kFrontierLanes;
 #pragma unroll
-                for (int j = 0; j < kSumTpt; ++j) {
-                    const int jj = min(j, n - 1 - i0);
-                    r[j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
+                    for (int j = 0; j < kSumTpt; ++j) {
+                        const int jj = min(j, n - 1 - i0);
+                        r[g][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
+                    }
+                } else {
+                    const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
+#pragma unroll
+                    for (int j = 0; j < kSumTpt; ++j) r[g][j] = src[min(j, n - 1 - i0)];
                 }
-            } else {
-                const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
-#pragma unroll
-                for (int j = 0; j < kSumTpt; ++j) r[j] = src[min(j, n - 1 - i0)];
             }
+        }
+    };
+    if (T > 0) gather(0);
+    for (int w0 = 0; w0 < T; w0 += kWin) {
+        const int n = min(kWin, T - w0);
+#ifdef SGMM_STAMPS
+        SGMM_SW(sw_a);
+#endif
+#pragma unroll
+        for (int g = 0; g < NT / TPB; ++g) {
+            const int i0 = (g * TPB + tid) * kSumTpt;
 #pragma unroll
             for (int j = 0; j < kSumTpt; ++j)
-                if (i0 + j < n) sel[i0 + j] = r[j];
-        }
+                if (i0 + j < n) sel[i0 + j] = r[g][j];
         }
         __syncthreads();
         SGMM_STAMP(e, 2);
+#ifdef SGMM_STAMPS
+        SGMM_SW(sw_b);
+        sw_g += sw_b - sw_a;
+#endif
+        if (w0 + kWin < T) gather(w0 + kWin);  // in flight during the sum
         S = exact_sum_window<NT>(sel, n, S, L);
+#ifdef SGMM_STAMPS
+        SGMM_SW(sw_a);
+        sw_s += sw_a - sw_b;
+        sw_n += 1;
+#endif
     }
+#ifdef SGMM_STAMPS
+    if (tid == 0 && e < 4096) {
+        g_stamps[e][11] = sw_g;
+        g_stamps[e][12] = sw_s;
+        g_stamps[e][15] = sw_n;
+    }
+#undef SGMM_SW
+#endif
     SGMM_STAMP(e, 3);
     int tr = 0;  // thread 0's record (the tails read it there only)
     double total = S;

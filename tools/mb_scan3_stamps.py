@@ -29,10 +29,11 @@ ticks = sg.TickStore(); s0 = ticks.add(tr, st); s1 = ticks.add(va, st); ticks.to
 params = sg.params_tensor([sg.EnvConfig(phi=1e-3, tick_size=0.001)], dev)
 pop = synthetic.population(K * P, H, sigma=0.05, seed=1).to(dev)
 gen, offs, lens = [], [], []
+VAL = not os.environ.get("TRAIN_ONLY")  # TRAIN_ONLY=1: the best-validation training launch
 for k in range(K):
-    gen += list(range(k * P, (k + 1) * P)) * 2
-    offs += [ticks.segments[s0][0]] * P + [ticks.segments[s1][0]] * P
-    lens += [4560] * P + [912] * P
+    gen += list(range(k * P, (k + 1) * P)) * (2 if VAL else 1)
+    offs += [ticks.segments[s0][0]] * P + ([ticks.segments[s1][0]] * P if VAL else [])
+    lens += [4560] * P + ([912] * P if VAL else [])
 n = len(gen)
 assert n <= 4096
 eb = sg.EpisodeBatch(np.array(gen), offs, lens, np.zeros(n)).to(dev)
@@ -45,6 +46,8 @@ L.sgmm_debug_stamps(h.ctypes.data, n)
 h = h.astype(np.int64)
 lens = np.array(lens)
 for name, m in (("train", lens == 4560), ("val", lens == 912)):
+    if not m.any():
+        continue
     x = h[m]
     rel = lambda k: np.median(x[:, k] - x[:, 0])
     print(f"{name}: cycles from entry (median): chunk-starts {rel(1):.0f}, last-window rewards {rel(2):.0f}, "
@@ -52,3 +55,10 @@ for name, m in (("train", lens == 4560), ("val", lens == 912)):
           f"walk iterations med {np.median(x[:, 13]):.0f}, fallback blocks med {np.median(x[:, 14]):.0f}")
     print(f"   entry spread (cycles, memtime): p10 {np.percentile(x[:, 0] - h[:, 0].min(), 10):.0f} "
           f"med {np.median(x[:, 0] - h[:, 0].min()):.0f} max {(x[:, 0] - h[:, 0].min()).max():.0f}")
+tot = (h[:, 3] - h[:, 0]).astype(float)
+print(f"  entry->end cycles: p10 {np.percentile(tot, 10):.0f} med {np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} max {tot.max():.0f}")
+print(f"  kernel span (memtime cycles): {(h[:, 3].max() - h[:, 0].min()):.0f}")
+g = h[:, 11].astype(float); sm = h[:, 12].astype(float); nw_ = h[:, 15].astype(float)
+print(f"  per episode summed over {np.median(nw_):.0f} windows: gather med {np.median(g):.0f} cycles, "
+      f"exact sum med {np.median(sm):.0f}; chunk starts med {np.median(h[:, 1] - h[:, 0]):.0f}; "
+      f"walk iterations med {np.median(h[:, 13]):.0f} fallback blocks med {np.median(h[:, 14]):.0f}")
