@@ -510,4 +510,112 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
     (void)la;
 }
 
+// The tell (tell_only) in a ONE-WAVE workgroup (the path scans above 1024
+// episodes): lane l holds records l, l + 64, ... (loaded 16 at a time, sc1),
+// the wave's argmax is a DPP maximum of the order-preserving key and a DPP
+// minimum of the index among equal keys (np.argmax: first index, NaN first),
+// the best's training record comes from its lane's registers, and the masters
+// are regenerated from up-front loads.  Same results as ga_step_dev.
+constexpr int kWaveRec = 16;     // records per lane loaded together
+constexpr int kWaveChunks = 8;   // float4 master chunks per lane: n <= 2048
+
+__device__ __forceinline__ int wave_min_i32(int v) {
+#define SGMM_MSTEP(CTRL, RM)                                                  \
+    {                                                                         \
+        const int t_ = (int)dpp32<CTRL, RM>((uint32_t)INT32_MAX, (uint32_t)v); \
+        v = t_ < v ? t_ : v;                                                  \
+    }
+    SGMM_MSTEP(0x111, 0xF) SGMM_MSTEP(0x112, 0xF) SGMM_MSTEP(0x114, 0xF)
+    SGMM_MSTEP(0x118, 0xF) SGMM_MSTEP(0x142, 0xA) SGMM_MSTEP(0x143, 0xC)
+#undef SGMM_MSTEP
+    return __builtin_amdgcn_readlane(v, kWave - 1);
+}
+
+// first index of the largest key over the wave (lane candidates (key, idx),
+// idx < 0: none); -1 when no lane has a candidate
+__device__ __forceinline__ int wave_best_index(uint64_t key, int idx) {
+    const uint64_t m = wave_max_u64(idx >= 0 ? key : 0ull);  // valid keys are > 0
+    const int c = wave_min_i32(idx >= 0 && key == m ? idx : INT32_MAX);
+    return c == INT32_MAX ? -1 : c;
+}
+
+__device__ __forceinline__ void regen_master_wave(float* __restrict__ master, int64_t n, float sig, uint64_t seed,
+                                                  uint32_t sid, uint32_t gen, int best) {
+    const int lane = threadIdx.x & (kWave - 1);
+    float m[kWaveChunks][4];
+#pragma unroll
+    for (int j = 0; j < kWaveChunks; ++j) {
+        const int64_t k4 = lane + (int64_t)j * kWave;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[j][q] = 4 * k4 + q < n ? master[4 * k4 + q] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < kWaveChunks; ++j) {
+        const int64_t k4 = lane + (int64_t)j * kWave;
+        if (4 * k4 >= n) break;
+        float z[4];
+        normal4(seed, sid, gen, (uint32_t)best, (uint32_t)k4, z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * k4 + q < n) master[4 * k4 + q] = m[j][q] + z[q] * sig;  // ask_row4's arithmetic
+    }
+}
+
+template <bool HANDOFF>
+__device__ void tell_wave(sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
+                          const int32_t* __restrict__ trades, int32_t P, float* __restrict__ master,
+                          float* __restrict__ master_adv, int64_t n_mm, int64_t n_adv, uint64_t seed,
+                          sgmm_ga_history* __restrict__ history, int32_t hist_cap) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int32_t gen_i = st->gen;
+    const uint32_t gen = (uint32_t)gen_i;
+    const float sig_mm = (float)st->sigma_mm, sig_adv = (float)st->sigma_adv;
+    // this lane's best (ascending indices: the first wins ties) for fit and
+    // -fit, over blocks of kWaveRec records per lane, each block's loads issued
+    // together
+    double bv = 0.0, av = 0.0;
+    int bi = -1, aj = -1;
+    int32_t btr = 0;
+    for (int r0 = 0; r0 * kWave < P; r0 += kWaveRec) {
+        double f[kWaveRec];
+        int32_t tr[kWaveRec];
+#pragma unroll
+        for (int r = 0; r < kWaveRec; ++r) {
+            const int i = lane + (r0 + r) * kWave;
+            f[r] = i < P ? ld_rec<HANDOFF>(fit + i) : 0.0;
+            tr[r] = (i < P && trades) ? ld_rec<HANDOFF>(trades + i) : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < kWaveRec; ++r) {
+            const int i = lane + (r0 + r) * kWave;
+            if (i < P) {
+                const bool tb = bi < 0 || better(f[r], i, bv, bi);
+                bv = tb ? f[r] : bv;
+                btr = tb ? tr[r] : btr;
+                bi = tb ? i : bi;
+                argmax_merge(av, aj, -f[r], i);
+            }
+        }
+    }
+    const int best = wave_best_index(argmax_key(bv), bi);
+    const int abest = wave_best_index(argmax_key(av), aj);
+    const int src = (best < 0 ? 0 : best) & (kWave - 1);
+    const double tf = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(bv), src));
+    const int32_t ttr = __builtin_amdgcn_readlane(btr, src);
+    // tell (model.py:73-76; drl_engine.py:119-125)
+    regen_master_wave(master, n_mm, sig_mm, seed, 0u, gen, best);
+    if (master_adv) regen_master_wave(master_adv, n_adv, sig_adv, seed, 1u, gen, abest);
+    if (lane == 0) {
+        st->best_idx = best;
+        st->adv_best_idx = abest;
+        st->last_train_f = tf;
+        if (history && gen_i < hist_cap) {
+            sgmm_ga_history* hist = history + gen_i;
+            hist->train_f = tf;
+            hist->train_trades = ttr;
+            hist->best_idx = best;
+        }
+    }
+}
+
 }  // namespace sgmm

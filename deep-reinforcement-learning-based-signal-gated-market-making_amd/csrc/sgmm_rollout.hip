@@ -1650,7 +1650,10 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
     float* lm = reinterpret_cast<float*>(si + 2 * nt);
     float* la = lm + sa.n_mm;
     const bool tell_only = sa.mode == 1;
-    if (sa.P <= nt && sa.n_mm <= 16 * nt && sa.n_adv <= 16 * nt)
+    if (tell_only && nt == kWave && sa.n_mm <= 4 * kWave * kWaveChunks && sa.n_adv <= 4 * kWave * kWaveChunks)
+        tell_wave<true>(sa.st, fitness, trades, sa.P, sa.master_mm, sa.master_adv, sa.n_mm, sa.n_adv, sa.seed,
+                        sa.history, sa.hist_cap);
+    else if (sa.P <= nt && sa.n_mm <= 16 * nt && sa.n_adv <= 16 * nt)
         ga_step_fused<true>(sa.st, fitness, trades, fitness + sa.P, trades + sa.P, sa.P, sa.master_mm,
                             sa.master_adv, sa.best_master, sa.n_mm, sa.n_adv, sa.seed, sa.history,
                             sa.hist_cap, sv, si, lm, la, tell_only);

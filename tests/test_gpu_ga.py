@@ -294,3 +294,23 @@ def test_drlengine_two_ranks_equal_one(sgmm, tmp_path):
             assert np.array_equal(o[k], np.array(hist[k], np.float64)), (r, k)
         assert np.array_equal(o["w"], pol.get_weights().numpy())
         assert float(o["sigma"]) == eng.mm_evolver.sigma
+
+
+def test_one_wave_tell_large_population(sgmm, tmp_path):
+    """P=1100 with best validation: 1 100 training episodes take one-wave path
+    scans, whose last workgroup runs the tell in one wave (tell_wave: records
+    loaded 16 per lane at a time, two blocks here, DPP argmax).  Fused
+    validation (2 200 episodes, the frontier kernel) gives the same run."""
+    tr, va, st = _bundles(11, T=400, Tv=100)
+    res = []
+    for val_mode in ("best", "fused"):
+        torch.manual_seed(4)
+        eng = sgmm.DRLEngine(pop_size=1100, phi=0.0005, tick_size=0.001, save_dir=str(tmp_path / val_mode),
+                             hidden_dim=16, rng="device", seed=21, val_mode=val_mode, verbose=False, sync_every=4,
+                             patience=2)
+        pol, hist = eng.train(tr, va, st, generations=8)
+        res.append((hist, pol.get_weights().numpy(), eng.mm_evolver.sigma))
+    (h0, w0, s0), (h1, w1, s1) = res
+    for k in h0:
+        assert np.array_equal(np.array(h0[k], np.float64), np.array(h1[k], np.float64), equal_nan=True), k
+    assert np.array_equal(w0, w1) and s0 == s1

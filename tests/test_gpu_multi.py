@@ -88,14 +88,16 @@ def test_multi_sweep_constructor_and_shared_bundle(sgmm, tmp_path):
 
 
 @pytest.mark.parametrize("P,arl,use_graph", [(24, False, True), (24, True, True), (300, False, False),
-                                             (300, True, True)])
+                                             (300, True, True), (400, False, True)])
 def test_best_validation_equals_fused(sgmm, tmp_path, P, arl, use_graph):
     """val_mode="best" (sgmm_generation_multi_best: training launch with the
     tell in its tail, then ONE validation episode per population on the new
     master, drl_engine.py:127-138) == val_mode="fused" (every individual
     validated inside the training launch, the best's record picked): the
     validation of the best is the same episode on the same genome, so the
-    histories, masters, sigma schedules and checkpoints agree bit for bit."""
+    histories, masters, sigma schedules and checkpoints agree bit for bit.
+    P=400: 1 200 training episodes take one-wave path scans, whose tell runs in
+    one wave (tell_wave); fused, 2 400 episodes run on the frontier kernel."""
     assets = _bundles()
     gens = 12
     tr = [assets[a][0] for _, _, a in POPS]

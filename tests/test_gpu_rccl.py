@@ -35,8 +35,14 @@ def nccl_world1():
         pytest.skip("no nccl (RCCL) backend")
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
-                            device_id=torch.device("cuda", 0))
+    for attempt in range(5):  # a probed free port can be taken before the store binds it
+        try:
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                                    device_id=torch.device("cuda", 0))
+            break
+        except dist.DistNetworkError:
+            if attempt == 4:
+                raise
     try:
         yield dist
     finally:

@@ -62,3 +62,8 @@ g = h[:, 11].astype(float); sm = h[:, 12].astype(float); nw_ = h[:, 15].astype(f
 print(f"  per episode summed over {np.median(nw_):.0f} windows: gather med {np.median(g):.0f} cycles, "
       f"exact sum med {np.median(sm):.0f}; chunk starts med {np.median(h[:, 1] - h[:, 0]):.0f}; "
       f"walk iterations med {np.median(h[:, 13]):.0f} fallback blocks med {np.median(h[:, 14]):.0f}")
+# the tell in the last-arriving workgroup of each population (generation launches only)
+t4, t5 = h[:, 4], h[:, 5]
+m = (t5 > t4) & (t4 > 0)
+if m.any():
+    print("  tail (last arrivers):", [(int(e), int(t5[e] - t4[e])) for e in np.where(m)[0][:8]])
