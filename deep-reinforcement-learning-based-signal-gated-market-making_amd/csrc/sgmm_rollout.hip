@@ -644,7 +644,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfm
 // single basic block.  Packed f32 FMAs are avoided beside the MFMAs (a
 // v_pk_fma_f32 there costs ~22 cycles more than two v_fma_f32).
 template <int H, int NSI, int MODE>
-__global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
+__global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k_policy_table_v3(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
     int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
     double* __restrict__ rew) {
@@ -673,29 +673,18 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
     const int64_t tix = tb + min(t0 + lane, T - 1);
     const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
     const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
-    __shared__ __attribute__((aligned(16))) float gsm[L::N];
+    // the genome is staged in the reward buffer: it is dead once every wave
+    // holds its weights in registers (the barrier below).  The LDS saved keeps
+    // the H = 16 workgroup at 30.8 KB, so five fit a CU (96 VGPRs: five waves
+    // per SIMD; config 2's table 21.3 -> 19.4 us)
+    __shared__ __attribute__((aligned(16))) double rl_s[4][NSI][kWave];  // [state][lane] path-plane rewards
+    static_assert(sizeof(rl_s) >= sizeof(float) * L::N, "genome fits the reward buffer");
+    float* gsm = reinterpret_cast<float*>(&rl_s[0][0][0]);
     stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
     __syncthreads();
     __shared__ __attribute__((aligned(16))) float w3i[2 * H];  // (W3[0][j], W3[1][j]) pairs
     if (threadIdx.x < 2 * H) w3i[threadIdx.x] = gsm[L::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
-    __syncthreads();
-    if (t0 >= T) return;  // wave-uniform; no block barriers below
-#ifdef SGMM_STAMPS
-    // slots: 7 realtime at entry, 0 start, 1 weights + layer 1 of state 0,
-    // 2 states done, 3 map scan, 4 end, 5 / 6 summed MFMA / vector blocks
-    const int wslot = e * (int)(gridDim.x * 4) + chunk;
-    unsigned long long st_m = 0, st_v = 0, st_a, st_b;
-#define SGMM_V3T(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
-#endif
-    SGMM_TSTAMP_REAL(wslot, 7);
-    SGMM_TSTAMP(wslot, 0, 0);
-    const sgmm_env_params p = params[ep.param[e]];
     const float* g = gsm;
-    __shared__ __attribute__((aligned(16))) float hb_s[4][kWave * HP];
-    float* hb = hb_s[wv];
-    __shared__ double rl_s[4][NSI][kWave];  // [state][lane] rewards for the path planes
-    double* rl = &rl_s[wv][0][0];
-
     float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
     f32x4 b2c[NT];      // C of layer 2: neurons 16rt + 4grp + r
 #pragma unroll
@@ -716,6 +705,21 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 4 : 2) void k_policy_table_v3(
         for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(a1, xs1[q], __builtin_fmaf(a0, xs0[q], bb));
     }
     const float b30 = g[L::B3], b31 = g[L::B3 + 1];
+    __syncthreads();      // the genome is dead: rl_s holds rewards from here
+    if (t0 >= T) return;  // wave-uniform; no block barriers below
+#ifdef SGMM_STAMPS
+    // slots: 7 realtime at entry, 0 start, 1 weights + layer 1 of state 0,
+    // 2 states done, 3 map scan, 4 end, 5 / 6 summed MFMA / vector blocks
+    const int wslot = e * (int)(gridDim.x * 4) + chunk;
+    unsigned long long st_m = 0, st_v = 0, st_a, st_b;
+#define SGMM_V3T(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+#endif
+    SGMM_TSTAMP_REAL(wslot, 7);
+    SGMM_TSTAMP(wslot, 0, 0);
+    const sgmm_env_params p = params[ep.param[e]];
+    __shared__ __attribute__((aligned(16))) float hb_s[4][kWave * HP];
+    float* hb = hb_s[wv];
+    double* rl = &rl_s[wv][0][0];
 
     f32x4 acc[MODE == 0 ? 2 : 1][4][NT];
     uint64_t map = kIdentityMap;
