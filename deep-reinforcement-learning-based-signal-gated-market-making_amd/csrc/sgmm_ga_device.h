@@ -317,16 +317,25 @@ constexpr int kTailSlots = 4;  // float4 master chunks per thread (n <= 16 * blo
 
 #ifdef SGMM_STAMPS
 static __device__ unsigned long long g_tail[8];  // diagnostic build: tail phase times (thread 0)
-#define SGMM_TAIL_STAMP(k, dep)                                                      \
-    do {                                                                             \
-        unsigned long long t_;                                                       \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" \
-                     : "=s"(t_) : "v"(dep) : "memory");                              \
-        if (threadIdx.x == 0) g_tail[k] = t_;                                        \
+#endif
+#if defined(SGMM_STAMPS) && !defined(SGMM_NO_TAIL_STAMPS)
+// the clock when `dep` is available (its register dependency only: no memory
+// wait), kept in registers and stored once at the end (SGMM_TAIL_FLUSH)
+#define SGMM_TAIL_DECL unsigned long long tt_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SGMM_TAIL_STAMP(k, dep) \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt_[k]) : "v"(dep) : "memory")
+#define SGMM_TAIL_FLUSH                                         \
+    do {                                                        \
+        if (threadIdx.x == 0)                                   \
+            for (int k_ = 0; k_ < 8; ++k_) g_tail[k_] = tt_[k_]; \
     } while (0)
 #else
+#define SGMM_TAIL_DECL
 #define SGMM_TAIL_STAMP(k, dep) \
     do {                        \
+    } while (0)
+#define SGMM_TAIL_FLUSH \
+    do {                \
     } while (0)
 #endif
 
@@ -382,6 +391,7 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
                               double* sv, int* si, float* lm, float* la, bool tell_only = false) {
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int nw = (nt + kWave - 1) / kWave;
+    SGMM_TAIL_DECL
     // ---- every load first
     double f = 0.0, vf = 0.0;
     int tr = 0, vtr = 0;
@@ -465,6 +475,7 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
                 hist->best_idx = best;
             }
         }
+        SGMM_TAIL_FLUSH;
         return;
     }
     if (tid == 0) {  // validation of the best (drl_engine.py:129-171)
@@ -506,6 +517,7 @@ __device__ void ga_step_fused(sgmm_ga_state* __restrict__ st, const double* __re
         }
     }
     SGMM_TAIL_STAMP(4, improved);
+    SGMM_TAIL_FLUSH;
     (void)lm;
     (void)la;
 }
