@@ -405,7 +405,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int H, int NSI, bool ARL>
-__global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : 1) void k_policy_table_mfma(
+__global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : (ARL ? 3 : 1)) void k_policy_table_mfma(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
     GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
     uint64_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
