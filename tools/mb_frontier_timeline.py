@@ -99,3 +99,15 @@ for lo, hi in ((0, 200), (200, 260), (260, 320), (320, 400), (400, 2000)):
     m = (simd_slots >= lo) & (simd_slots < hi)
     if m.any():
         print(f"    SIMDs with {lo}-{hi} slots: {m.sum():4d}, last end med {np.median(last[m]) / 1e3:.1f} max {last[m].max() / 1e3:.1f} us")
+# what packing the (chunk, state) pairs densely into the 64 columns would save
+pk = h[:, 4].astype(float); pt = h[:, 5].astype(float); ts = h[:, 3].astype(float)
+for name, m in (("train", lens == 4560), ("val", lens == 912)):
+    if not m.any():
+        continue
+    print(f"  packed {name}: slots {sl[m].sum():.0f} -> {pk[m].sum():.0f}, tile-slots {ts[m].sum():.0f} -> {pt[m].sum():.0f}")
+hs = np.argsort(-sl)[:16]
+print("  heaviest waves (slots, packed slots, tile-slots, packed tile-slots):",
+      [(int(sl[w]), int(pk[w]), int(ts[w]), int(pt[w])) for w in hs])
+for q in (50, 90, 99):
+    w = np.argsort(sl)[int(len(sl) * q / 100) - 1]
+    print(f"  p{q} wave: slots {int(sl[w])} packed {int(pk[w])} tile-slots {int(ts[w])} packed {int(pt[w])}")
