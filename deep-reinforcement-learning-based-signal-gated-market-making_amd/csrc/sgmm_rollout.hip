@@ -405,7 +405,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int H, int NSI, bool ARL>
-__global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : (ARL ? 3 : 1)) void k_policy_table_mfma(
+__global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : ((ARL && H <= 32) ? 3 : 1)) void k_policy_table_mfma(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
     GenomeSrc src, int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr,
     uint64_t* __restrict__ cmaps, uint64_t* __restrict__ fills, double* __restrict__ rew) {
@@ -887,6 +887,14 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
 // the other chunks track every state in [inv_min, inv_max].  Arithmetic per
 // (tick, state) is the table's (same MFMA chains, same fp64 step), so every
 // output bit is the table's.
+template <int N>
+struct IntC {
+    static constexpr int value = N;
+};
+// number of lanes below this one whose bit is set in m
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
 constexpr int kFrontierMaxWaves = 2;   // waves (64-chunk groups) per episode
 constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunk slots per episode
@@ -943,6 +951,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
     __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
     __shared__ __attribute__((aligned(16))) float b2s[H];
+#ifndef SGMM_FRONTIER_NOPACK
+    // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
+    // successor (bits 9-11) and the fill (bit 12) written back by the column
+    __shared__ uint16_t pl[kWave * (NSI - 1)];
+#endif
     float* gsm = reinterpret_cast<float*>(big);
     stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
     __syncthreads();
@@ -981,7 +994,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #ifdef SGMM_STAMPS
     // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
     // slots and tile-slots run (slots 2, 3); nothing inside the loop waits
-    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0;
+    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_pk = 0, lite_pt = 0;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
 #endif
 #ifdef SGMM_STAMPS_PHASE
@@ -1014,6 +1027,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
         if (!act) fmask = 0;
+#ifdef SGMM_FRONTIER_NOPACK
         // slots per 16-lane tile: the most frontier states of any of its lanes
         // (a row maximum in four DPP steps -- pairs, quads, half rows, rows --
         // instead of four dependent LDS permutes)
@@ -1029,6 +1043,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #ifdef SGMM_STAMPS
         lite_sl += nslot;
         lite_ts += tsl[0] + tsl[1] + tsl[2] + tsl[3];
+#endif
+#endif
+#ifdef SGMM_STAMPS
+        {
+            // what (chunk, state) pairs packed densely into the 64 columns would need
+            int so = __builtin_popcount(fmask);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) so += __shfl_xor(so, m, kWave);
+            lite_pk += (so + 63) / 64;
+            lite_pt += (so + 15) / 16;
+        }
 #endif
         // the weights stay in LDS: an opaque base per tick keeps the compiler
         // from hoisting ~90 loop-invariant weight loads into registers
@@ -1060,9 +1085,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         SGMM_FT(fs_b);
         fs_c[5] += fs_b - fs_a;
 #endif
-        uint32_t rem = fmask;
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
         uint32_t trm = 0;                 // bit f: a fill from frontier state f
+#ifdef SGMM_FRONTIER_NOPACK
+        // slot k = the k-th frontier state of every lane (max occupancy slots)
+        uint32_t rem = fmask;
 #pragma unroll 1
         for (int k = 0; k < nslot; ++k) {
             lds_cf* w3p = (lds_cf*)(&w3i[0]);
@@ -1181,6 +1208,225 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             }
 #endif
         }
+#else
+        // Slot 0: each lane's first frontier state in its own column (the
+        // common case: most ticks have one state per chunk).  Slots 1..: the
+        // remaining (chunk, state) pairs packed densely into the 64 columns --
+        // a chunk whose paths stay apart costs its extra states, not extra
+        // slots for the whole wave.  Each column computes with its pair's own
+        // inputs (the chunk's signals and prices, the state's inventory), so
+        // every (tick, state) result is bit-identical to the unpacked walk.
+        const uint32_t ext = fmask & (fmask - 1u);  // frontier states after the first
+        const uint32_t nex = (uint32_t)__builtin_popcount(ext);
+        const uint64_t eb0 = __ballot(nex & 1u), eb1 = __ballot(nex & 2u), eb2 = __ballot(nex & 4u);
+        const int epfx = mbcnt64(eb0) + 2 * mbcnt64(eb1) + 4 * mbcnt64(eb2);  // first pair of this lane
+        const int etot = __popcll(eb0) + 2 * __popcll(eb1) + 4 * __popcll(eb2);  // extra pairs (uniform)
+        {
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    pl[pp++] = (uint16_t)((lane << 3) | __builtin_ctz(r));
+                    r &= r - 1u;
+                }
+        }
+        const bool any0 = __ballot(fmask != 0u) != 0ull;
+        const int nx = (etot + kWave - 1) / kWave;
+#ifdef SGMM_STAMPS
+        lite_sl += (any0 ? 1 : 0) + nx;
+        lite_ts += (any0 ? 4 : 0) + (etot + 15) / 16;
+#endif
+        // layers 1-3 of the four 16-column tiles' samples (tiles >= NQ skipped):
+        // x2q / pq = inv / 2 and the layer-1 signal terms of sample 16q + col
+        auto mlp = [&](auto nq, const float(&x2q)[4], const float(&pq)[4][KS], float& o0, float& o1) {
+            constexpr int NQ = decltype(nq)::value;
+            lds_cf* w3p = (lds_cf*)(&w3i[0]);
+            asm volatile("" : "+v"(w3p));
+            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
+            asm volatile("" : "+v"(w1p));
+            lds_cf* b2p = (lds_cf*)(&b2s[0]);
+            asm volatile("" : "+v"(b2p));
+            // layer 1 + layer 2: 4 x NT independent accumulator chains issued
+            // k-step by k-step keep the matrix pipe busy
+            f32x4 acc[4][NT];
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) {
+                const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q][rt] = bb;
+            }
+#pragma unroll
+            for (int i4 = 0; i4 < KS; i4 += 4) {
+                const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pq[q][i4 + r]));
+#pragma unroll
+                        for (int rt = 0; rt < NT; ++rt)
+                            acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
+                    }
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                SGMM_FT(t_);  // MFMAs issued (not completed)
+                fs_c[1] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+                }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[2] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+            // layer 3 of this lane's column, in neuron order (the canonical chain)
+            o0 = w3p[2 * H];
+            o1 = w3p[2 * H + 1];
+#pragma unroll 1
+            for (int j8 = 0; j8 < H / 8; ++j8) {
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j4 = 2 * j8 + jj;
+                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+                    for (int r2 = 0; r2 < 2; ++r2) {
+                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
+                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                    }
+                }
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[3] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        };
+        if (any0) {
+            float x2q[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
+                x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
+            }
+            float o0, o1;
+            mlp(IntC<4>{}, x2q, pre, o0, o1);
+            const bool has = fmask != 0u;
+            const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
+            if (has) {
+                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
+                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
+                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
+                rl[f * kWave + lane] = so1.reward;
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[4] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        }
+#pragma unroll 1
+        for (int x = 0; x < nx; ++x) {
+            // column lane = pair 64 x + lane: (chunk lane src, state f)
+            const int pidx = kWave * x + lane;
+            const bool has = pidx < etot;
+            const uint32_t v = has ? (uint32_t)pl[pidx] : 0u;
+            const int src = (int)(v >> 3);
+            const uint32_t f = v & 7u;
+            float x2q[4], pq[4][KS];
+            {
+                float xs0[4], xs1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t vq = (uint32_t)__shfl((int)v, 16 * q + col, kWave);
+                    const int sq = (int)(vq >> 3);
+                    x2q[q] = (float)(inv_min + (int)(vq & 7u)) * 0.5f;
+                    xs0[q] = __shfl(s1, sq, kWave);
+                    xs1[q] = __shfl(s2, sq, kWave);
+                }
+                lds_cf* l1q = (lds_cf*)(&l1w[0][0]);
+                asm volatile("" : "+v"(l1q));
+#pragma unroll
+                for (int i = 0; i < KS; ++i) {
+                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1q + 4 * (4 * i + grp));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) pq[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
+                }
+            }
+            const int ntile = min(4, (etot - kWave * x + 15) >> 4);
+            float o0, o1;
+            if (ntile == 1)
+                mlp(IntC<1>{}, x2q, pq, o0, o1);
+            else if (ntile == 2)
+                mlp(IntC<2>{}, x2q, pq, o0, o1);
+            else
+                mlp(IntC<4>{}, x2q, pq, o0, o1);
+            // the FPT step with the pair's chunk's prices
+            const double smid = __shfl(tmid, src, kWave), sask = __shfl(task, src, kWave);
+            const double sbid = __shfl(tbid, src, kWave), sbmax = __shfl(tbmax, src, kWave);
+            const double ssmin = __shfl(tsmin, src, kWave);
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, smid, sask, sbid, sbmax, ssmin);
+            if (has) {
+                rl[f * kWave + src] = so1.reward;
+                const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
+                pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[4] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        }
+        {
+            // the owner lane collects its extra states' successors and fills
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    const uint32_t f = (uint32_t)__builtin_ctz(r);
+                    r &= r - 1u;
+                    const uint32_t w = pl[pp++];
+                    stepmap = (stepmap & ~(0xFFull << (8 * f))) | ((uint64_t)((w >> 9) & 7u) << (8 * f));
+                    trm |= ((w >> 12) & 1u) << f;
+                }
+        }
+#endif
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_b);
 #endif
@@ -1244,6 +1490,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             g_tstamps[e][1] = t1;
             g_tstamps[e][2] = lite_sl;
             g_tstamps[e][3] = lite_ts;
+            g_tstamps[e][4] = lite_pk;
+            g_tstamps[e][5] = lite_pt;
             g_thwid[e][0] = h_;
             g_thwid[e][1] = x_;
         }
