@@ -2461,11 +2461,14 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
 // How many episodes run as one wave in the frontier kernel (the longest
 // fwhole of the order); the rest are split into two waves (two 64-chunk
 // groups of half the length, at the cost of more start-state paths to
-// merge).  A whole episode is a long serial walk and every SIMD holds three
-// waves (occupancy), so the split count evens the load: 3 x SIMDs units, e.g.
-// 2560 episodes on 1024 SIMDs -> 2048 whole + 512 split = 3072 waves, two
-// whole and one half episode per SIMD instead of 512 SIMDs with three whole
-// episodes.  SGMM_FRONTIER_NW=1|2 forces all whole / all split.
+// merge).  Default: every episode whole.  SGMM_FRONTIER_NW=2 splits all,
+// SGMM_FRONTIER_NW=3 balances to 3 x SIMDs waves (every SIMD holds three
+// waves: 2560 episodes on 1024 SIMDs -> 2048 whole + 512 split = 3072 waves).
+// The balance won before the packed extra slots (config 3: 727-736 vs 753 us
+// policy kernel); with packing, all-whole gives the faster generation over a
+// 100-generation run (659 vs 670 us, tools/gpu_nw2.sh): a split episode's
+// second group tracks all five start states until they merge, and packing
+// does not remove that work.
 static int simd_count() {
     static int n = 0;
     if (n == 0) {
@@ -2478,10 +2481,10 @@ static int simd_count() {
     return n;
 }
 static int32_t frontier_whole(int32_t n) {
-    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
-        if (std::atoi(v) == 1) return n;
-        if (std::atoi(v) == 2) return 0;
-    }
+    const char* v = std::getenv("SGMM_FRONTIER_NW");
+    const int mode = v ? std::atoi(v) : 1;
+    if (mode == 2) return 0;
+    if (mode != 3) return n;
     const int64_t split = std::min<int64_t>(n, std::max<int64_t>(0, 3LL * simd_count() - n));
     return (int32_t)(n - split);
 }

@@ -80,10 +80,11 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
     assert np.array_equal(fit, wf)
 
 
-@pytest.mark.parametrize("nw", ["", "1", "2"], ids=["default", "1wave", "2waves"])
+@pytest.mark.parametrize("nw", ["", "1", "2", "3"], ids=["default", "1wave", "2waves", "balanced"])
 def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
     """From 2048 episodes on the frontier kernel is the default: 2100 ragged
-    episodes bit-exact against the oracle."""
+    episodes bit-exact against the oracle (balanced: 972 of them split into
+    two waves, the rest whole, in one launch)."""
     if nw:
         monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
     lens = 300 + (np.arange(2100) * 37) % 900
