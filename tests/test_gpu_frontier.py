@@ -133,3 +133,20 @@ def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
     for k in ha:
         assert np.array_equal(np.array(ha[k], np.float64), np.array(hb[k], np.float64), equal_nan=True), k
     assert np.array_equal(wa, wb)
+
+
+@pytest.mark.parametrize("nw", ["1", "2"], ids=["1wave", "2waves"])
+def test_frontier_one_wave_scan_row_gather(sgmm, oracle, monkeypatch, nw):
+    """Above 1024 episodes the path scan is one wave per episode and gathers
+    windows of W = 1024 // CL whole chunks row by row (consecutive lanes =
+    consecutive chunks of a plane row): W from 2 to past 64, the per-lane
+    4-tick gather once CL > 512 (W < 2), ragged last windows and chunks,
+    both chunk groups of split episodes -- bit-exact against the oracle."""
+    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
+    monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
+    base = np.array([17, 255, 4560, 8191, 20001, 30003, 40000, 4097])
+    n = 1100
+    lens = base[np.arange(n) % len(base)] + (np.arange(n) // len(base)) % 7
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=51, sigma=0.3)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
