@@ -951,11 +951,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
     __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
     __shared__ __attribute__((aligned(16))) float b2s[H];
-#ifndef SGMM_FRONTIER_NOPACK
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
     // successor (bits 9-11) and the fill (bit 12) written back by the column
     __shared__ uint16_t pl[kWave * (NSI - 1)];
-#endif
     float* gsm = reinterpret_cast<float*>(big);
     stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
     __syncthreads();
@@ -1027,24 +1025,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
         if (!act) fmask = 0;
-#ifdef SGMM_FRONTIER_NOPACK
-        // slots per 16-lane tile: the most frontier states of any of its lanes
-        // (a row maximum in four DPP steps -- pairs, quads, half rows, rows --
-        // instead of four dependent LDS permutes)
-        int ns = __builtin_popcount(fmask);
-        ns = max(ns, (int)dpp32<0xB1>(0u, (uint32_t)ns));   // quad_perm [1,0,3,2]
-        ns = max(ns, (int)dpp32<0x4E>(0u, (uint32_t)ns));   // quad_perm [2,3,0,1]
-        ns = max(ns, (int)dpp32<0x141>(0u, (uint32_t)ns));  // row_half_mirror
-        ns = max(ns, (int)dpp32<0x140>(0u, (uint32_t)ns));  // row_mirror
-        int tsl[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) tsl[q] = __builtin_amdgcn_readlane(ns, 16 * q);
-        const int nslot = max(max(tsl[0], tsl[1]), max(tsl[2], tsl[3]));
-#ifdef SGMM_STAMPS
-        lite_sl += nslot;
-        lite_ts += tsl[0] + tsl[1] + tsl[2] + tsl[3];
-#endif
-#endif
 #ifdef SGMM_STAMPS
         {
             // what (chunk, state) pairs packed densely into the 64 columns would need
@@ -1087,128 +1067,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #endif
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
         uint32_t trm = 0;                 // bit f: a fill from frontier state f
-#ifdef SGMM_FRONTIER_NOPACK
-        // slot k = the k-th frontier state of every lane (max occupancy slots)
-        uint32_t rem = fmask;
-#pragma unroll 1
-        for (int k = 0; k < nslot; ++k) {
-            lds_cf* w3p = (lds_cf*)(&w3i[0]);
-            asm volatile("" : "+v"(w3p));
-            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
-            asm volatile("" : "+v"(w1p));
-            lds_cf* b2p = (lds_cf*)(&b2s[0]);
-            asm volatile("" : "+v"(b2p));
-            const bool has = rem != 0u;
-            const uint32_t f = has ? (uint32_t)__builtin_ctz(rem) : 0u;
-            rem &= rem - 1u;
-            // layer 1 + layer 2 for all four 16-lane tiles and both 16-neuron
-            // halves: 4 x NT independent accumulator chains issued k-step by
-            // k-step keep the matrix pipe busy (a tile-by-tile schedule waits
-            // ~40 cycles on every dependent MFMA); tiles without a k-th state
-            // compute and discard (they are the exception: 5.2 of 5.4 tile-slots run)
-            f32x4 acc[4][NT];
-            {
-                // inv / 2 of sample 16q + col's k-th state (exact in float: |inv| <= 8)
-                float x2q[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
-                    remq[q] &= remq[q] - 1u;
-                    x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
-                }
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt) {
-                    const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[q][rt] = bb;
-                }
-#pragma unroll
-                for (int i4 = 0; i4 < KS; i4 += 4) {
-                    const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pre[q][i4 + r]));
-#pragma unroll
-                            for (int rt = 0; rt < NT; ++rt)
-                                acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
-                        }
-                }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                SGMM_FT(t_);  // MFMAs issued (not completed)
-                fs_c[1] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt) {
-                    f32x4 v;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
-                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
-                }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[2] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-            // layer 3 of this lane's sample, in neuron order (the canonical chain)
-            float o0 = w3p[2 * H], o1 = w3p[2 * H + 1];
-#pragma unroll 1
-            for (int j8 = 0; j8 < H / 8; ++j8) {
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int j4 = 2 * j8 + jj;
-                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
-#pragma unroll
-                    for (int r2 = 0; r2 < 2; ++r2) {
-                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
-                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
-                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
-                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
-                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
-                    }
-                }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[3] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
-            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
-            if (has) {
-                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
-                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
-                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
-                rl[f * kWave + lane] = so1.reward;
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[4] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        }
-#else
         // Slot 0: each lane's first frontier state in its own column (the
         // common case: most ticks have one state per chunk).  Slots 1..: the
         // remaining (chunk, state) pairs packed densely into the 64 columns --
@@ -1426,7 +1284,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
                     trm |= ((w >> 12) & 1u) << f;
                 }
         }
-#endif
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_b);
 #endif
