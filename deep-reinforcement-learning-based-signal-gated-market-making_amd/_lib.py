@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading libsgmm.so, see module doc)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("SGMM_LIB", PKG_DIR / "libsgmm.so"))
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class SgmmError(RuntimeError):
@@ -105,6 +105,7 @@ SIGNATURES = {
     "sgmm_policy_forward": (ctypes.c_int, [_VP, _I64, _I32, _VP, _VP, _VP, _I64, _VP]),
     "sgmm_adversary_forward": (ctypes.c_int, [_VP, _I64, _VP, _VP, _VP, _I64, _VP]),
     "sgmm_rollout_workspace_size": (_SZ, [_I32, _I64, _I32]),
+    "sgmm_rollout_workspace_bytes": (_SZ, [_I32, _I64, _I32, _I32]),
     "sgmm_rollout_fitness": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,
                                             _VP, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _SZ, _VP]),
     "sgmm_rollout_trace": (ctypes.c_int, [ctypes.POINTER(Ticks), ctypes.POINTER(Episodes), _VP,

@@ -203,6 +203,7 @@ extern "C" int sgmm_ga_step_multi(const sgmm_populations* pops, const double* fi
     SGMM_REQUIRE(pops->states && pops->masters_mm && pops->seeds && fitness && val_fitness, "null pointer");
     SGMM_REQUIRE(shard_n <= 0 || shard_stride >= 8LL * shard_n, "shard_stride < 8 * shard_n");
     const int64_t n_mm = (int64_t)pops->hidden * pops->hidden + 7 * pops->hidden + 2;
+    SGMM_REQUIRE(n_mm <= kMaxStepParams, "genome too large for the GA step");  // the LDS master stage
     PopsArg pa{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, pops->seeds,
                pops->history, pops->history_cap, pops->P, n_mm, pops->masters_adv ? 1250 : 0};
     ProfScope prof("ga_step", as_stream(stream));

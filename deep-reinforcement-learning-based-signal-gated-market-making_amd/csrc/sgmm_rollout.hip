@@ -2291,14 +2291,31 @@ static size_t ws_ctr(int32_t n, int64_t steps) {
 static size_t ws_kinfo(int32_t n) { return align256((n_frontier_slots(n) + n) * sizeof(uint32_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
+// The workspace of a batch with n_inventory inventory values, with or
+// without the adversary (then 4 * n_inventory states: inventory x previous
+// fill flags).  The adversary flag is explicit: 4 * n_inventory <= 8 for one
+// or two inventory values, so a state count alone cannot tell the layouts apart.
+static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t nsi, bool arl) {
+    if (total_steps < 0 || nsi <= 0 || nsi > 8 || n_episodes < 0) return 0;
+    if (arl)  // fill codes, chunk transducers, per-state planes rew[state * rs + row]
+        return ws_fills(total_steps) + align256(n_chunk_slots(n_episodes, total_steps) * kArlSlot) +
+               (size_t)rew_stride(total_steps, n_episodes) * (size_t)(4 * nsi) * sizeof(double);
+    return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
+           (size_t)rew_stride(total_steps, n_episodes) * (size_t)nsi * sizeof(double);
+}
+
+extern "C" size_t sgmm_rollout_workspace_bytes(int32_t n_episodes, int64_t total_steps, int32_t n_inventory,
+                                               int32_t with_adversary) {
+    return rollout_ws_bytes(n_episodes, total_steps, n_inventory, with_adversary != 0);
+}
+
+// ABI 3 form: n_states > 8 means the adversary layout with n_states / 4
+// inventory values (use sgmm_rollout_workspace_bytes for an adversary batch
+// with fewer than 3 inventory values)
 extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps,
                                               int32_t n_states) {
-    if (total_steps < 0 || n_states <= 0 || n_episodes < 0) return 0;
-    if (n_states > 8)  // adversary: fill codes, chunk transducers, per-state planes rew[state * rs + row]
-        return ws_fills(total_steps) + align256(n_chunk_slots(n_episodes, total_steps) * kArlSlot) +
-               (size_t)rew_stride(total_steps, n_episodes) * (size_t)n_states * sizeof(double);
-    return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           (size_t)rew_stride(total_steps, n_episodes) * (size_t)n_states * sizeof(double);
+    if (n_states > 8) return n_states % 4 ? 0 : rollout_ws_bytes(n_episodes, total_steps, n_states / 4, true);
+    return rollout_ws_bytes(n_episodes, total_steps, n_states, false);
 }
 
 // Frontier kernel or table: the frontier kernel does ~1/3 of the table's
@@ -2451,7 +2468,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     if (eps->n == 0) return SGMM_OK;
     const int32_t nsi = eps->inv_max - eps->inv_min + 1;
     const int32_t ns = arl ? 4 * nsi : nsi;
-    const size_t need = sgmm_rollout_workspace_size(eps->n, eps->total_steps, ns);
+    const size_t need = rollout_ws_bytes(eps->n, eps->total_steps, nsi, arl);
     if (!workspace || workspace_bytes < need) {
         set_error("workspace %zu bytes < required %zu", workspace_bytes, need);
         return SGMM_ERR_WORKSPACE;

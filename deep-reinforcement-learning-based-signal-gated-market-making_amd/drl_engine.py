@@ -120,12 +120,15 @@ def evaluate_individual(mm_weights, adv_weights, bundle, phi, tick_size, fee_rat
 
 
 def _dist_info(dist):
+    """(group, rank, world, group_active): group_active is False for one
+    process -- dist=False, or no process group initialised -- even when a
+    default group exists, so the session never touches that group."""
     if dist is False:
-        return None, 0, 1
+        return None, 0, 1, False
     if torch.distributed.is_available() and torch.distributed.is_initialized():
         g = dist if dist not in (None, True) else None
-        return g, torch.distributed.get_rank(g), torch.distributed.get_world_size(g)
-    return None, 0, 1
+        return g, torch.distributed.get_rank(g), torch.distributed.get_world_size(g), True
+    return None, 0, 1, False
 
 
 class DRLEngine:
@@ -141,7 +144,8 @@ class DRLEngine:
       val_mode    -- "fused": validate every individual in the training launch and
                      pick the best's value (removes a serial episode per generation);
                      "best": validate only the best after tell (reference order);
-                     "auto": fused for shards of <= 512 individuals.
+                     "auto": best from BEST_VAL_MIN_SHARD (256) individuals per
+                     population shard, fused below.
       honor_sigma -- the reference ignores DRLEngine(sigma=...) (NeuroEvolution keeps
                      its 0.05 default, drl_engine.py:77); True uses it.
       sync_every  -- generations between host synchronisations (log lines and
@@ -238,8 +242,8 @@ class _GraphedGenerations:
         if not self.sharded:
             return True
         import torch.distributed as tdist
-        if not (tdist.is_available() and tdist.is_initialized()):
-            return True  # one process without a group: the gather is a device copy
+        if not (self.group_active and tdist.is_available() and tdist.is_initialized()):
+            return True  # one process (no group, or dist=False): the gather is a device copy
         return tdist.get_backend(self.group) == "nccl"
 
     def capture(self):
@@ -320,7 +324,7 @@ class TrainingSession(_GraphedGenerations):
         self.roll = RolloutEngine(eng.device or "cuda")
         dev = self.dev = self.roll.device
         self.L = self.roll.L
-        self.group, self.rank, self.world = _dist_info(eng.dist)
+        self.group, self.rank, self.world, self.group_active = _dist_info(eng.dist)
         self.sharded = self.world > 1 or eng.exchange == "always"
         P, H = eng.pop_size, eng.hidden_dim
         self.P, self.H, self.G = P, H, genome_size(H)
@@ -351,7 +355,8 @@ class TrainingSession(_GraphedGenerations):
 
         g_tr, o_tr, l_tr = phase(tr_off, self.T_tr)
         g_va, o_va, l_va = phase(va_off, self.T_va)
-        self.rec = FitnessRecords(P, self.world, dev, gather=self.sharded, with_val=not self.best_step)
+        self.rec = FitnessRecords(P, self.world, dev, gather=self.sharded, with_val=not self.best_step,
+                                  group_active=self.group_active)
         if self.fused:  # one launch: training + validation episodes of the shard
             adv = np.concatenate([g_tr, np.full(n_cap, -1)]) if arl else None  # validation: no adversary
             self.train_eps = EpisodeBatch(np.concatenate([g_tr, g_va]), np.concatenate([o_tr, o_va]),
@@ -656,7 +661,7 @@ class MultiSession(_GraphedGenerations):
         self.roll = RolloutEngine(e0.device or "cuda")
         dev = self.dev = self.roll.device
         self.L = self.roll.L
-        self.group, self.rank, self.world = _dist_info(e0.dist)
+        self.group, self.rank, self.world, self.group_active = _dist_info(e0.dist)
         self.sharded = self.world > 1 or e0.exchange == "always"
         P, H = self.P, self.H = e0.pop_size, e0.hidden_dim
         G = self.G = genome_size(H)
@@ -706,7 +711,8 @@ class MultiSession(_GraphedGenerations):
             if self.best_val else None
         self.vout = (torch.zeros(K, dtype=torch.float64, device=dev),
                      torch.zeros(K, dtype=torch.int32, device=dev)) if self.best_val else None
-        self.rec = FitnessRecords(P, self.world, dev, n_pop=K, gather=self.sharded, with_val=not self.best_val)
+        self.rec = FitnessRecords(P, self.world, dev, n_pop=K, gather=self.sharded, with_val=not self.best_val,
+                                  group_active=self.group_active)
         f32 = dict(dtype=torch.float32, device=dev)
         self.masters = torch.stack([e.mm_evolver.master_policy.get_weights() for e in engs]).to(**f32).contiguous()
         self.masters_adv = torch.stack([e.adv_evolver.master_policy.get_weights() for e in engs]).to(**f32) \

@@ -151,8 +151,8 @@ class RolloutEngine:
         self._ws = None
 
     def workspace_bytes(self, eps: EpisodeBatch, arl: bool) -> int:
-        ns = (eps.inv_max - eps.inv_min + 1) * (4 if arl else 1)
-        return int(self.L.sgmm_rollout_workspace_size(eps.n, eps.total_steps, ns))
+        nsi = eps.inv_max - eps.inv_min + 1
+        return int(self.L.sgmm_rollout_workspace_bytes(eps.n, eps.total_steps, nsi, 1 if arl else 0))
 
     def reserve(self, eps: EpisodeBatch, arl: bool):
         """Grow the workspace for this batch now (never inside a graph capture:

@@ -62,11 +62,16 @@ class FitnessRecords:
     results alone, f64 fitness[K][n] then i32 trades[K][n] (12 K n bytes)."""
 
     def __init__(self, P: int, world: int, device, n_pop: int = 1, gather: bool | None = None,
-                 with_val: bool = True):
+                 with_val: bool = True, group_active: bool = True):
         # gather: keep a gathered buffer and exchange even at world 1 (the
-        # sharded path rehearsed on one process); default: world > 1
+        # sharded path rehearsed on one process); default: world > 1.
+        # group_active: the session runs over a process group (DRLEngine(dist=False)
+        # is one process even when a default group exists: the gather is then a copy)
         self.P, self.world, self.K = int(P), int(world), int(n_pop)
         self.sharded = bool(world > 1 if gather is None else gather)
+        self.group_active = bool(group_active)
+        if self.world > 1 and not self.group_active:
+            raise ValueError("a world of several ranks needs a process group")
         self.with_val = bool(with_val)
         n = self.n = shard_capacity(P, world)
         K = self.K
@@ -90,7 +95,8 @@ class FitnessRecords:
         import torch.distributed as dist
         if not self.sharded:
             return
-        if not (dist.is_available() and dist.is_initialized()):  # one process, no group: the gather is a copy
+        if not (self.group_active and dist.is_available() and dist.is_initialized()):
+            # one process (no group, or the session opted out of it): the gather is a copy
             self.gathered.copy_(self.rec)
             return
         if self.device.type == "cuda" and dist.get_backend(group) == "gloo":

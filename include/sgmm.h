@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SGMM_ABI_VERSION 3
+#define SGMM_ABI_VERSION 4
 
 enum {
     SGMM_OK = 0,
@@ -125,7 +125,14 @@ int sgmm_adversary_forward(const float *genomes, int64_t genome_stride,
                            const int32_t *genome_idx, const float *states, float *out,
                            int64_t n, void *stream);
 
-/* Workspace bytes sgmm_rollout_fitness needs for this batch. */
+/* Workspace bytes sgmm_rollout_fitness needs for this batch: n_inventory =
+ * inv_max - inv_min + 1 inventory values, with_adversary != 0 when the batch
+ * runs adversaries (adv_genomes / masters_adv non-NULL). (ABI 4) */
+size_t sgmm_rollout_workspace_bytes(int32_t n_episodes, int64_t total_steps, int32_t n_inventory,
+                                    int32_t with_adversary);
+/* ABI 3 form: n_states = n_inventory, or 4 * n_inventory with the adversary
+ * -- read as the adversary layout only when > 8, so an adversary batch with
+ * fewer than 3 inventory values must be sized with sgmm_rollout_workspace_bytes. */
 size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_steps, int32_t n_states);
 
 /* THE HOT PATH.  Fitness of every episode of the batch:

@@ -67,9 +67,13 @@ static int32_t act_to_int(float r)
     return (int32_t)r;
 }
 
-/* ReLU on the bit pattern, max(bits, 0) as int32 -- the kernels' v_max_i32.
- * Identical to torch's relu for every non-NaN input; NaN pre-activations
- * (only NaN state inputs produce them) are outside the parity domain. */
+/* ReLU on the bit pattern, max(bits, 0) as int32.  The kernels use
+ * v_med3_f32(a, 0, +inf) instead (sgmm_device.h relu); the two agree for every
+ * non-NaN input except the sign of a zero (-0.0 -> +0.0 here, -0.0 or +0.0
+ * there), which changes no dot product's value beyond the sign of an exact
+ * zero and so no action.  Both equal torch's relu on non-NaN inputs; NaN
+ * pre-activations (only NaN state inputs produce them) are outside the
+ * parity domain, where the two forms may differ. */
 static float relu32(float a)
 {
     int32_t b;

@@ -67,6 +67,67 @@ def records_rank(rank, world, port, P, outdir):
         dist.destroy_process_group()
 
 
+MULTI_POPS = [(0.0001, 0.001, 0), (0.005, 0.001, 0), (0.01, 0.01, 1)]  # (phi, tick, asset) per population
+
+
+def multi_workload():
+    """Per-population (train, val, stats) lists: two assets with their own
+    tick sizes and lengths, as tests/test_gpu_multi.py."""
+    from sgmm_amd import synthetic
+    a_tr, a_va = synthetic.bundle_510300(600, seed=10), synthetic.bundle_510300(150, seed=11)
+    b_tr, b_va = synthetic.bundle_688981(520, seed=12), synthetic.bundle_688981(170, seed=13)
+    assets = ((a_tr, a_va, synthetic.train_stats(a_tr)), (b_tr, b_va, synthetic.train_stats(b_tr)))
+    return ([assets[a][j] for _, _, a in MULTI_POPS] for j in range(3))
+
+
+def multi_engines(sg, P, arl, save_dir, val_mode, dist=None):
+    import torch
+    engines = []
+    for k, (phi, tick, _) in enumerate(MULTI_POPS):
+        torch.manual_seed(100 + k)  # the initial masters come from the torch generator
+        engines.append(sg.DRLEngine(pop_size=P, phi=phi, tick_size=tick, use_arl=arl, save_dir=save_dir,
+                                    hidden_dim=16, rng="device", seed=1000 + 7 * k, val_mode=val_mode,
+                                    sync_every=5, patience=3, verbose=False, dist=dist))
+    return sg.MultiDRLEngine(engines)
+
+
+def multi_result(multi, res):
+    """Histories, final masters, adversary masters and sigmas of every population."""
+    out = {}
+    for k, (pol, hist) in enumerate(res):
+        e = multi.engines[k]
+        out[f"w{k}"] = pol.get_weights().numpy()
+        out[f"sigma{k}"] = np.float64(e.mm_evolver.sigma)
+        if e.use_arl:
+            out[f"adv{k}"] = e.adv_evolver.master_policy.get_weights().numpy()
+            out[f"asigma{k}"] = np.float64(e.adv_evolver.sigma)
+        for key, v in hist.items():
+            out[f"h{k}_{key}"] = np.array(v, np.float64)
+    return out
+
+
+def multi_train_rank(rank, world, port, P, gens, outdir, val_mode, arl, table_path=""):
+    """MultiDRLEngine (3 populations, two assets) over `world` ranks sharing one
+    GPU: every population's shard rolled out per rank, one gloo all-gather of
+    the K records, then the multi-population tell/validation (best) or GA
+    step (fused) on the gathered records -- the cross-rank record addressing
+    (i / n) * K * record + k * stride + (i % n) * size with i / n > 0."""
+    if table_path:
+        os.environ["SGMM_TABLE_PATH"] = table_path
+    dist = _setup(rank, world, port)
+    try:
+        import sgmm_pkg
+        sg = sgmm_pkg.load()
+        tr, va, st = multi_workload()
+        multi = multi_engines(sg, P, arl, os.path.join(outdir, f"ck{rank}"), val_mode)
+        sess = multi.session(tr, va, st, generations=gens)
+        assert sess.world == world and sess.sharded and sess.best_val == (val_mode == "best")
+        res = multi.train(tr, va, st, generations=gens)
+        np.savez(os.path.join(outdir, f"m{rank}.npz"), **multi_result(multi, res))
+    finally:
+        dist.destroy_process_group()
+
+
 def train_rank(rank, world, port, P, gens, outdir, backend="gloo"):
     """DRLEngine over `world` ranks sharing one GPU (gloo exchange staged
     through host memory): saves the history and the final master."""

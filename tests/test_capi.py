@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(sgmm):
     assert declared <= exported, declared - exported
     assert exported <= declared, exported - declared  # nothing undocumented
     assert set(_lib.SIGNATURES) == declared            # the binding covers the header
-    assert L.sgmm_abi_version() == 3
+    assert L.sgmm_abi_version() == 4
 
 
 def test_struct_layouts_match_header(sgmm):
@@ -58,6 +58,13 @@ def test_argument_errors_need_no_gpu(sgmm):
     assert rc == -1 and b"null" in L.sgmm_last_error()
     rc = L.sgmm_policy_forward(ctypes.c_void_p(8), 370, 12, None, ctypes.c_void_p(8), ctypes.c_void_p(8), 1, None)
     assert rc == -1 and b"hidden" in L.sgmm_last_error()
+    # H = 64 genomes (4546 floats) overflow the GA step's LDS master stage: rejected
+    # before launch by every multi-population GA entry point
+    v = ctypes.c_void_p(8)
+    pops = _lib.Populations(1, 8, 64, 0, 8, 8, None, None, 8, None)
+    for rc in (L.sgmm_ga_step_multi(ctypes.byref(pops), v, v, v, v, 0, 0, 0, 0, None),
+               L.sgmm_ga_tell_multi(ctypes.byref(pops), v, v, 0, 0, 0, 0, None)):
+        assert rc == -1 and b"genome too large" in L.sgmm_last_error()
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
     # frontier kernel (128 chunk slots per episode: u64 map, u32[8] counts, u32 merge info;
@@ -76,6 +83,15 @@ def test_argument_errors_need_no_gpu(sgmm):
     # adversary (20 states): u64 fill words + 64-byte chunk transducers (1000/64 + 4 + 1 slots)
     # + per-state f64 reward planes (stride 1000 + 512 * 4 rounded to 32)
     assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 3072 * 8
+    # ABI 4: the adversary flag is explicit, so 1 or 2 inventory values (4 or 8
+    # states) get the adversary layout, not the no-adversary one of the same state count
+    assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 1) == L.sgmm_rollout_workspace_size(4, 1000, 20)
+    assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) == L.sgmm_rollout_workspace_size(4, 1000, 5)
+    for nsi in (1, 2):
+        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 1280 + 4 * nsi * 3072 * 8
+    # the worked example: one 5000-tick ARL episode with 2 inventory values
+    assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) > L.sgmm_rollout_workspace_size(1, 5000, 8)
+    assert L.sgmm_rollout_workspace_bytes(4, 1000, 9, 0) == 0  # more than 8 inventory values
 
 
 def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):

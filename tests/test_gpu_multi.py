@@ -131,3 +131,54 @@ def test_best_validation_equals_fused(sgmm, tmp_path, P, arl, use_graph):
         b = torch.load(os.path.join(tmp_path / "best", name), weights_only=True)
         assert all(torch.equal(a[x], b[x]) for x in b), k
     assert any(f < 0.05 for f in (e.mm_evolver.sigma for e in mb.engines))  # patience 3: a decay happened
+
+
+@pytest.mark.parametrize("world,P,val_mode,arl,table_path", [
+    (2, 25, "best", False, ""),
+    (2, 25, "fused", True, ""),
+    (3, 25, "best", True, ""),
+    (3, 25, "fused", False, ""),
+    (2, 25, "best", False, "frontier"),
+], ids=["w2-best", "w2-fused-arl", "w3-best-arl", "w3-fused", "w2-best-frontier"])
+def test_multi_sharded_ranks_equal_one_process(sgmm, tmp_path, world, P, val_mode, arl, table_path):
+    """MultiDRLEngine over `world` ranks (gloo exchange, every rank on this GPU;
+    P=25 does not divide by 2 or 3, so the last shard is short) equals the
+    one-process MultiDRLEngine bit for bit: histories, final masters, adversary
+    masters, sigma schedules and rank 0's checkpoints.  Each rank reads
+    individual i of population k from the gathered records at
+    (i / n) * K * record + k * stride + (i % n) * size, so shards i / n > 0 are
+    read across ranks (sgmm_ga_tell_multi + sgmm_validate_multi with best
+    validation, sgmm_ga_step_multi fused; Env/drl_engine.py:91-125)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    import _shard_ranks as R
+    gens = 8
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    mp.spawn(R.multi_train_rank, args=(world, port, P, gens, str(tmp_path), val_mode, arl, table_path),
+             nprocs=world, join=True)
+    tr, va, st = R.multi_workload()
+    old = os.environ.get("SGMM_TABLE_PATH")
+    if table_path:
+        os.environ["SGMM_TABLE_PATH"] = table_path
+    try:
+        single = R.multi_engines(sgmm, P, arl, str(tmp_path / "single"), val_mode, dist=False)
+        want = R.multi_result(single, single.train(tr, va, st, generations=gens))
+    finally:
+        if old is None:
+            os.environ.pop("SGMM_TABLE_PATH", None)
+        else:
+            os.environ["SGMM_TABLE_PATH"] = old
+    for r in range(world):
+        got = np.load(tmp_path / f"m{r}.npz")
+        assert sorted(got.files) == sorted(want), r
+        for key in want:
+            assert np.array_equal(got[key], want[key], equal_nan=True), (r, key)
+    for k, (phi, _, _) in enumerate(R.MULTI_POPS):
+        name = f"agent_best_val_{phi}.pth"
+        a = torch.load(os.path.join(tmp_path / "ck0", name), weights_only=True)
+        b = torch.load(os.path.join(tmp_path / "single", name), weights_only=True)
+        assert all(torch.equal(a[x], b[x]) for x in b), k
+    # the populations trained and differ
+    assert len({float(want[f"h{k}_train_f"][-1]) for k in range(len(R.MULTI_POPS))}) == len(R.MULTI_POPS)

@@ -349,3 +349,39 @@ def test_ordered_sum_matches_sequential(sgmm, name, init, x):
         assert np.isnan(got)
     else:
         assert got.tobytes() == np.float64(want).tobytes(), (name, got, want)
+
+
+@pytest.mark.parametrize("caps", [(0, 0), (0, -1), (1, 0)], ids=["1inv", "2inv_neg", "2inv_pos"])
+def test_adversary_small_inventory_ranges(sgmm, oracle, caps):
+    """Adversarial episodes with 1 or 2 inventory values (4 or 8 states of
+    (inventory, previous fills)): the workspace takes the adversary layout
+    (sgmm_rollout_workspace_bytes' explicit flag; a state count of 4 or 8
+    alone reads as the no-adversary layout) and every episode is bit-exact
+    against the oracle, 5000-tick episodes included."""
+    i_max, i_min = caps
+    from sgmm_amd import synthetic
+    T, H, P = 5000, 16, 5
+    b = synthetic.bundle_510300(T, seed=41)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=0.5, seed=42)
+    rng = np.random.default_rng(43)
+    adv = (rng.standard_normal((P, 1250)) * 2).astype(np.float32)
+    lens = np.array([T, 1, 63, 777, 4096])
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.001, tick_size=0.001, i_max=i_max, i_min=i_min)], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
+                           adv=np.arange(P), inv_min=i_min, inv_max=i_max).to(DEV)
+    eng = sgmm.RolloutEngine(DEV)
+    nsi = i_max - i_min + 1
+    assert eng.workspace_bytes(eb, True) == eng.L.sgmm_rollout_workspace_bytes(eb.n, eb.total_steps, nsi, 1)
+    fit, trd = eng.fitness(ticks, eb, params, pop.to(DEV), H, torch.from_numpy(adv).to(DEV))
+    fit, trd = fit.cpu().numpy(), trd.cpu().numpy()
+    p = oracle.params(phi=0.001, tick=0.001, i_max=i_max, i_min=i_min)
+    for i in range(P):
+        L = int(lens[i])
+        f, t = oracle.evaluate(pop[i].numpy(), H, adv[i], s1n[:L], s2n[:L], b[2][:L], b[3][:L], b[4][:L],
+                               b[5][:L], b[6][:L], p)
+        assert trd[i] == t and fit[i] == f, (caps, L, fit[i], f)
