@@ -77,12 +77,16 @@ def parse():
     ap.add_argument("--hidden", type=int, default=0, help="override: TradingPolicy hidden width")
     ap.add_argument("--ticks", type=int, default=0, help="override: training ticks")
     ap.add_argument("--val-ticks", type=int, default=-1, help="override: validation ticks")
-    ap.add_argument("--profile-steps", type=int, default=5,
-                    help="eager generations timed kernel by kernel with HIP events")
+    ap.add_argument("--profile-steps", type=int, default=0,
+                    help="timed-window generations re-run eagerly and timed kernel by kernel with HIP events "
+                         "(0: all of them)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-episodes", type=int, default=64, help="episodes in the CPU-baseline sample")
     ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest for this config)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="strong-scaled configs (4, 5): run ONE rank's shard of an N-GPU run on this GPU "
+                         "(ceil(P/N) individuals per population; no exchange) and label the line '1 of N ranks'")
     ap.add_argument("--val-mode", default="auto", choices=("auto", "fused", "best"),
                     help="DRLEngine val_mode (auto: best from 256 individuals per population shard)")
     return ap.parse_args()
@@ -203,6 +207,16 @@ def latest_pmc(path_arg, config):
         return None
 
 
+def _series(per_gen, kname, g0):
+    """One kernel's per-generation time over the profiled window: first, last,
+    mean, min, max (us) and the generations they cover."""
+    us = [1e3 * d[kname][0] / d[kname][1] for d in per_gen if kname in d]
+    if not us:
+        return None
+    return {"generations": [g0, g0 + len(us) - 1], "first": us[0], "last": us[-1], "mean": sum(us) / len(us),
+            "min": min(us), "max": max(us)}
+
+
 def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, val_mode, seed0=1234):
     import torch
     torch.manual_seed(seed0)
@@ -238,6 +252,11 @@ def main():
     from sgmm_amd.shard import shard_capacity
 
     P, H, T, Tv = spec["P"], spec["H"], spec["T"], spec["Tv"]
+    shard_of = max(1, args.shard_of)
+    if shard_of > 1:
+        if spec["scaling"] != "strong" or world > 1:
+            raise SystemExit("--shard-of applies to the strong-scaled configs (4, 5) on one process")
+        P = shard_capacity(P, shard_of)  # one rank's shard of the N-GPU run
     P_glob = P * world if spec["scaling"] == "weak" else P
     K = len(spec["pops"])
     data = bundles(spec)
@@ -271,26 +290,37 @@ def main():
     ms_per_step = dt / args.steps * 1e3
     value = K * P_glob * T * args.steps / dt
 
-    # per-kernel durations: eager generations of this rank's shard; the library
-    # hands each profiled kernel a pair of HIP events recorded by its own
+    # per-kernel durations over the TIMED window: the same generations re-run
+    # eagerly on this rank's shard with the timed run's seeds (so the identical
+    # populations), every kernel handed a pair of HIP events recorded by its own
     # dispatch on the launch stream (hipExtLaunchKernel, sgmm_profile_*); graph
-    # replays launch the identical kernels
+    # replays launch the identical kernels.  The policy kernel gets cheaper as
+    # the populations train, so its first / last / mean over the window are
+    # reported and the mean is the roofline's launch time.
     n_rank = shard_capacity(P_glob, world)
+    g0 = args.warmup
+    n_prof = args.steps if args.profile_steps <= 0 else min(args.steps, max(args.profile_steps, 1))
     peng = make_engine(sgmm, spec, n_rank, tmp, False, False, args.val_mode)  # the timed run's seeds
-    psess = peng.session(tr, va, st, generations=args.profile_steps + 2)
-    psess.step(0)
-    psess.step(1)
+    psess = peng.session(tr, va, st, generations=g0 + n_prof)
+    for g in range(g0):
+        psess.step(g)
     torch.cuda.synchronize()
     _lib.profile_read()
     _lib.profile_enable(True)
-    for g in range(2, 2 + args.profile_steps):
+    per_gen = []
+    for g in range(g0, g0 + n_prof):
         psess.step(g)
-    torch.cuda.synchronize()
+        per_gen.append(_lib.profile_read())
     _lib.profile_enable(False)
-    prof = _lib.profile_read()
     psess.finish()
+    prof = {}
+    for d in per_gen:
+        for k, (ms, cnt) in d.items():
+            a = prof.setdefault(k, [0.0, 0])
+            a[0] += ms
+            a[1] += cnt
     kernels = {k: {"avg_us": 1e3 * v[0] / v[1], "launches": v[1]} for k, v in prof.items()}
-    gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, args.profile_steps)
+    gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, n_prof)
 
     # roofline of the policy kernel (the FP32 compute kernel of the path): the
     # frontier kernel from 2048 episodes per launch, the table below that
@@ -298,7 +328,8 @@ def main():
     # the training launch: training episodes (+ every validation episode when fused)
     steps_per_launch = K * n_rank * (T if best_val else T + Tv)
     fl = flop_per_step(H)
-    kname = "policy_frontier" if "policy_frontier" in kernels else "policy_table"
+    kname = next((k for k in ("policy_frontier_scan", "policy_frontier", "policy_table") if k in kernels),
+                 "policy_table")
     tab = kernels.get(kname)
     pmc = latest_pmc(args.pmc, args.config)
     roofline = None
@@ -309,17 +340,21 @@ def main():
             traffic = pmc["kernels"][kname].get("hbm_bytes_per_launch")
         note = ("algorithmic = one policy forward per env-step ("
                 + ("training" if best_val else "training + validation") + " ticks of one launch). "
-                + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.35 per "
-                   "training tick on this workload, in 16-lane MFMA tiles)" if kname == "policy_frontier" else
-                   "k_policy_table_v3 evaluates every inventory state (5x this work)"))
+                + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.2-1.35 per "
+                   "training tick on this workload, in 16-lane MFMA tiles)" if kname.startswith("policy_frontier") else
+                   "k_policy_table_v3 evaluates every inventory state (5x this work)")
+                + ("; the launch also runs every episode's path scan and the GA tell (fused: the time is walk + "
+                   "scan + tell)" if kname == "policy_frontier_scan" else ""))
         roofline = {"bound": "mfma", "pipe": "fp32 (gfx950 f32 MFMA peak == f32 VALU peak)",
-                    "kernel": ("k_policy_frontier" if kname == "policy_frontier" else
+                    "kernel": ("k_policy_frontier<fused scans>" if kname == "policy_frontier_scan" else
+                               "k_policy_frontier" if kname == "policy_frontier" else
                                "k_policy_table_mfma (adversary)" if spec["arl"] else "k_policy_table_v3"),
                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
                     "algorithmic": {"flop_per_env_step": fl, "env_steps_per_launch": steps_per_launch,
                                     "note": note},
-                    "avg_launch_us": tab["avg_us"]}
+                    "avg_launch_us": tab["avg_us"],
+                    "launch_us_over_timed_window": _series(per_gen, kname, g0)}
         if traffic:
             gbps = traffic / (tab["avg_us"] * 1e-6) / 1e9
             roofline["hbm"] = {"achieved_GBps": gbps, "peak_GBps": HBM_PEAK_GBPS,
@@ -333,7 +368,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": spec["scaling"], "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
-            "config": {"workload": describe(spec, world, P_glob, best_val), "config_id": args.config,
+            "config": {"workload": describe(spec, world, P_glob, best_val) + (
+                           f"; ONE RANK'S SHARD: 1 of {shard_of} ranks (ceil(P/{shard_of}) = {P} individuals per "
+                           f"population, rollout + tell on this GPU, no exchange)" if shard_of > 1 else ""),
+                       "config_id": args.config, "shard_of": shard_of,
                        "populations": K, "population_global": P_glob, "population_per_gpu": n_rank,
                        "phis": [p for p, _, _ in spec["pops"]], "hidden": H, "ticks_train": T, "ticks_val": Tv,
                        "adversary": spec["arl"], "val_mode": "best" if best_val else "fused",

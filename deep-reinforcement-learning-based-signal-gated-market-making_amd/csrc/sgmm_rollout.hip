@@ -898,6 +898,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
 constexpr int kFrontierMaxWaves = 2;   // waves (64-chunk groups) per episode
 constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunk slots per episode
+constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
 typedef __attribute__((address_space(3))) const float lds_cf;
 typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
 // ticks per chunk with nw waves (64 nw chunks) per episode
@@ -906,466 +907,16 @@ __host__ __device__ __forceinline__ int frontier_len(int T, int nw) {
     return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
 }
 // the episode's block of plane rows: nw groups of frontier_len(T, nw) x 64 rows
-// <= T + 256 nw slots (T rounded up to 64 nw chunks of a multiple of 4), so
-// blocks at step_off + 512 e never overlap; the plane stride covers
-// total_steps + 512 n (rew_stride).  Group g's row of tick offset u, lane l:
-// base + g * CL * 64 + u * 64 + l (tick-offset-major within the group)
+// <= T + 512 rows (T rounded up to 64 nw chunks of a multiple of 4), starting
+// on a 128-byte line (16 rows), so blocks at step_off + 528 e (rounded up to
+// 16) never overlap and no two episodes share a line -- a scan of the fused
+// launch may read its episode while a neighbour's walk still writes; the plane
+// stride covers total_steps + 528 n (rew_stride).  Group g's row of tick
+// offset u, lane l: base + g * CL * 64 + u * 64 + l (tick-offset-major within
+// the group)
+constexpr int kFrontierPad = 4 * kFrontierSlots + 16;  // plane rows per episode beyond its ticks
 __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
-    return step_off + (int64_t)4 * kFrontierSlots * e;
-}
-
-template <int H, int NSI>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(
-    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
-    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ cmaps, uint32_t* __restrict__ ctr32,
-    uint32_t* __restrict__ kinfo, double* __restrict__ rew) {
-    static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
-    using L = GenomeLayout<H>;
-    constexpr int NT = H / 16, KS = H / 4;
-    constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
-    // wave b: the whole episode at order position b (b < fwhole), else chunk
-    // group g of a split episode (two waves each, longest episodes first)
-    const int b = (int)blockIdx.x;
-    const int pos = b < ep.fwhole ? b : ep.fwhole + ((b - ep.fwhole) >> 1);
-    const int nw = b < ep.fwhole ? 1 : 2, cg = b < ep.fwhole ? 0 : (b - ep.fwhole) & 1;
-    const int e = ep.order ? ep.order[pos] : pos;
-    if (cg == 0 && threadIdx.x == 0) ep.fnw[e] = (uint32_t)nw;
-    const int32_t T = ep.len[e];
-    if (T <= 0) return;  // block-uniform
-    const int CL = frontier_len(T, nw);
-    const int nch = (T + CL - 1) / CL;
-    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
-    const int lane = threadIdx.x, grp = lane >> 4, col = lane & 15;
-    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
-    const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
-    const int t0 = c * CL;
-    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
-
-    // LDS (~9 KB per wave, so 3 waves per SIMD fit): the genome is staged in
-    // `big`, the weights the loop needs are copied out, then `big` holds the
-    // half-activation transpose buffer and the per-state rewards
-    constexpr int kBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
-    __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
-    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 4];  // (W3[0][j], W3[1][j]) pairs, then b3
-    __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
-    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
-    __shared__ __attribute__((aligned(16))) float b2s[H];
-    // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
-    // successor (bits 9-11) and the fill (bit 12) written back by the column
-    __shared__ uint16_t pl[kWave * (NSI - 1)];
-    float* gsm = reinterpret_cast<float*>(big);
-    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
-    __syncthreads();
-    if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
-    if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
-    if (lane < H) {
-        w1x[lane & 3][lane >> 2] = gsm[L::W1 + 3 * lane + 2];
-        l1w[lane][0] = gsm[L::W1 + 3 * lane];
-        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
-        l1w[lane][2] = gsm[L::B1 + lane];
-        l1w[lane][3] = gsm[L::W1 + 3 * lane + 2];
-        b2s[lane] = gsm[L::B2 + lane];
-    }
-    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
-#pragma unroll
-    for (int rt = 0; rt < NT; ++rt)
-#pragma unroll
-        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
-    __syncthreads();  // gsm is dead from here: big becomes hb + rl
-    float* hb = reinterpret_cast<float*>(big);                          // [64][HP]
-    double* rl = reinterpret_cast<double*>(big + kWave * HP * 4);       // [NSI][64]
-    const sgmm_env_params p = params[ep.param[e]];
-
-    // per-lane path bookkeeping: byte s of cur = the state of the path that
-    // started the chunk in state s (tracked starts: bits of sset)
-    const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
-    const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
-    uint64_t cur = kIdentityMap;
-    uint32_t cnt[NSI];
-#pragma unroll
-    for (int s = 0; s < NSI; ++s) cnt[s] = 0;
-    bool merged = __builtin_popcount(sset) <= 1;
-    int kc = merged ? 0 : CL;
-    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
-#ifdef SGMM_STAMPS
-    // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
-    // slots and tile-slots run (slots 2, 3); nothing inside the loop waits
-    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_pk = 0, lite_pt = 0;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
-#endif
-#ifdef SGMM_STAMPS_PHASE
-    // per wave (episode): 0 cycles, 1 layers 1-2 (MFMA issue), 2 relu + transpose
-    // (MFMA drain), 3 layer 3, 4 FPT step, 5 per-tick head (frontier, signals,
-    // layer-1 terms), 6 planes, 7 wall time (10 ns ticks)
-    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
-#define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
-    SGMM_FT(fs_t0);
-#endif
-    int64_t ti = tick_of(0);
-    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
-#pragma unroll 1
-    for (int tt = 0; tt < CL; ++tt) {
-#ifdef SGMM_STAMPS_PHASE
-        SGMM_FT(fs_a);
-#endif
-        const bool act = tt < ntl;
-        const float s1 = ns1, s2 = ns2;
-        // this tick's prices: first used after the tick's MLP, which hides the load
-        const double tmid = tk.mid_next[ti], task = tk.best_ask[ti], tbid = tk.best_bid[ti];
-        const double tbmax = tk.buy_max[ti], tsmin = tk.sell_min[ti];
-        ti = tick_of(tt + 1);
-        ns1 = tk.s1n[ti];
-        ns2 = tk.s2n[ti];
-        // frontier: the distinct current states of the tracked paths
-        uint32_t fmask = 0;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s)
-            if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
-        if (!act) fmask = 0;
-#ifdef SGMM_STAMPS
-        {
-            // what (chunk, state) pairs packed densely into the 64 columns would need
-            int so = __builtin_popcount(fmask);
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) so += __shfl_xor(so, m, kWave);
-            lite_pk += (so + 63) / 64;
-            lite_pt += (so + 15) / 16;
-        }
-#endif
-        // the weights stay in LDS: an opaque base per tick keeps the compiler
-        // from hoisting ~90 loop-invariant weight loads into registers
-        lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
-        asm volatile("" : "+v"(l1p));
-        // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
-        float pre[4][KS];
-        // the frontier of each B-operand sample's chunk (lane 16q + col): the
-        // slots take their k-th state from it, no per-slot permute
-        uint32_t remq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) remq[q] = (uint32_t)__shfl((int)fmask, 16 * q + col, kWave);
-        {
-            float xs0[4], xs1[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xs0[q] = __shfl(s1, 16 * q + col, kWave);
-                xs1[q] = __shfl(s2, 16 * q + col, kWave);
-            }
-#pragma unroll
-            for (int i = 0; i < KS; ++i) {
-                const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
-#pragma unroll
-                for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
-            }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        SGMM_FT(fs_b);
-        fs_c[5] += fs_b - fs_a;
-#endif
-        uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
-        uint32_t trm = 0;                 // bit f: a fill from frontier state f
-        // Slot 0: each lane's first frontier state in its own column (the
-        // common case: most ticks have one state per chunk).  Slots 1..: the
-        // remaining (chunk, state) pairs packed densely into the 64 columns --
-        // a chunk whose paths stay apart costs its extra states, not extra
-        // slots for the whole wave.  Each column computes with its pair's own
-        // inputs (the chunk's signals and prices, the state's inventory), so
-        // every (tick, state) result is bit-identical to the unpacked walk.
-        const uint32_t ext = fmask & (fmask - 1u);  // frontier states after the first
-        const uint32_t nex = (uint32_t)__builtin_popcount(ext);
-        const uint64_t eb0 = __ballot(nex & 1u), eb1 = __ballot(nex & 2u), eb2 = __ballot(nex & 4u);
-        const int epfx = mbcnt64(eb0) + 2 * mbcnt64(eb1) + 4 * mbcnt64(eb2);  // first pair of this lane
-        const int etot = __popcll(eb0) + 2 * __popcll(eb1) + 4 * __popcll(eb2);  // extra pairs (uniform)
-        {
-            uint32_t r = ext;
-            int pp = epfx;
-#pragma unroll
-            for (int m = 0; m < NSI - 1; ++m)
-                if (r) {
-                    pl[pp++] = (uint16_t)((lane << 3) | __builtin_ctz(r));
-                    r &= r - 1u;
-                }
-        }
-        const bool any0 = __ballot(fmask != 0u) != 0ull;
-        const int nx = (etot + kWave - 1) / kWave;
-#ifdef SGMM_STAMPS
-        lite_sl += (any0 ? 1 : 0) + nx;
-        lite_ts += (any0 ? 4 : 0) + (etot + 15) / 16;
-#endif
-        // layers 1-3 of the four 16-column tiles' samples (tiles >= NQ skipped):
-        // x2q / pq = inv / 2 and the layer-1 signal terms of sample 16q + col
-        auto mlp = [&](auto nq, const float(&x2q)[4], const float(&pq)[4][KS], float& o0, float& o1) {
-            constexpr int NQ = decltype(nq)::value;
-            lds_cf* w3p = (lds_cf*)(&w3i[0]);
-            asm volatile("" : "+v"(w3p));
-            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
-            asm volatile("" : "+v"(w1p));
-            lds_cf* b2p = (lds_cf*)(&b2s[0]);
-            asm volatile("" : "+v"(b2p));
-            // layer 1 + layer 2: 4 x NT independent accumulator chains issued
-            // k-step by k-step keep the matrix pipe busy
-            f32x4 acc[4][NT];
-#pragma unroll
-            for (int rt = 0; rt < NT; ++rt) {
-                const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) acc[q][rt] = bb;
-            }
-#pragma unroll
-            for (int i4 = 0; i4 < KS; i4 += 4) {
-                const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pq[q][i4 + r]));
-#pragma unroll
-                        for (int rt = 0; rt < NT; ++rt)
-                            acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
-                    }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                SGMM_FT(t_);  // MFMAs issued (not completed)
-                fs_c[1] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt) {
-                    f32x4 v;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
-                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
-                }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[2] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-            // layer 3 of this lane's column, in neuron order (the canonical chain)
-            o0 = w3p[2 * H];
-            o1 = w3p[2 * H + 1];
-#pragma unroll 1
-            for (int j8 = 0; j8 < H / 8; ++j8) {
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int j4 = 2 * j8 + jj;
-                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
-#pragma unroll
-                    for (int r2 = 0; r2 < 2; ++r2) {
-                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
-                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
-                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
-                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
-                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
-                    }
-                }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[3] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        };
-        if (any0) {
-            float x2q[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
-                x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
-            }
-            float o0, o1;
-            mlp(IntC<4>{}, x2q, pre, o0, o1);
-            const bool has = fmask != 0u;
-            const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
-            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
-            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
-            if (has) {
-                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
-                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
-                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
-                rl[f * kWave + lane] = so1.reward;
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[4] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        }
-#pragma unroll 1
-        for (int x = 0; x < nx; ++x) {
-            // column lane = pair 64 x + lane: (chunk lane src, state f)
-            const int pidx = kWave * x + lane;
-            const bool has = pidx < etot;
-            const uint32_t v = has ? (uint32_t)pl[pidx] : 0u;
-            const int src = (int)(v >> 3);
-            const uint32_t f = v & 7u;
-            float x2q[4], pq[4][KS];
-            {
-                float xs0[4], xs1[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t vq = (uint32_t)__shfl((int)v, 16 * q + col, kWave);
-                    const int sq = (int)(vq >> 3);
-                    x2q[q] = (float)(inv_min + (int)(vq & 7u)) * 0.5f;
-                    xs0[q] = __shfl(s1, sq, kWave);
-                    xs1[q] = __shfl(s2, sq, kWave);
-                }
-                lds_cf* l1q = (lds_cf*)(&l1w[0][0]);
-                asm volatile("" : "+v"(l1q));
-#pragma unroll
-                for (int i = 0; i < KS; ++i) {
-                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1q + 4 * (4 * i + grp));
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) pq[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
-                }
-            }
-            const int ntile = min(4, (etot - kWave * x + 15) >> 4);
-            float o0, o1;
-            if (ntile == 1)
-                mlp(IntC<1>{}, x2q, pq, o0, o1);
-            else if (ntile == 2)
-                mlp(IntC<2>{}, x2q, pq, o0, o1);
-            else
-                mlp(IntC<4>{}, x2q, pq, o0, o1);
-            // the FPT step with the pair's chunk's prices
-            const double smid = __shfl(tmid, src, kWave), sask = __shfl(task, src, kWave);
-            const double sbid = __shfl(tbid, src, kWave), sbmax = __shfl(tbmax, src, kWave);
-            const double ssmin = __shfl(tsmin, src, kWave);
-            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
-            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, smid, sask, sbid, sbmax, ssmin);
-            if (has) {
-                rl[f * kWave + src] = so1.reward;
-                const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
-                pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[4] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        }
-        {
-            // the owner lane collects its extra states' successors and fills
-            uint32_t r = ext;
-            int pp = epfx;
-#pragma unroll
-            for (int m = 0; m < NSI - 1; ++m)
-                if (r) {
-                    const uint32_t f = (uint32_t)__builtin_ctz(r);
-                    r &= r - 1u;
-                    const uint32_t w = pl[pp++];
-                    stepmap = (stepmap & ~(0xFFull << (8 * f))) | ((uint64_t)((w >> 9) & 7u) << (8 * f));
-                    trm |= ((w >> 12) & 1u) << f;
-                }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        SGMM_FT(fs_b);
-#endif
-        // the tick's rewards along the tracked paths; once they have merged only plane p0
-        if (act) {
-            // planes in tick-offset-major order (row u of an episode's block holds
-            // the 64 chunks' rewards at offset u): one coalesced 512-byte store
-            // per plane and tick; row-major rows made every 8-byte store a
-            // partial line and the L2 wrote ~6x the bytes back
-            const int64_t row = rbase + (int64_t)tt * kFrontierLanes + lane;
-#pragma unroll
-            for (int s = 0; s < NSI; ++s) {
-                if (!((sset >> s) & 1u)) continue;
-                const uint32_t st = map_get(cur, (uint32_t)s);
-                if (!merged || (uint32_t)s == p0) rew[s * ep.rs + row] = rl[st * kWave + lane];
-                cnt[s] += (trm >> st) & 1u;
-            }
-            cur = map_then(cur, stepmap);
-            if (!merged) {
-                uint32_t fm = 0;
-#pragma unroll
-                for (int s = 0; s < NSI; ++s)
-                    if ((sset >> s) & 1u) fm |= 1u << map_get(cur, (uint32_t)s);
-                if (__builtin_popcount(fm) <= 1) {
-                    merged = true;
-                    kc = tt + 1;
-                }
-            }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        {
-            unsigned long long t_;
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            SGMM_FT(t_);
-            fs_c[6] += t_ - fs_b;
-        }
-#endif
-    }
-#ifdef SGMM_STAMPS_PHASE
-    {
-        unsigned long long t_;
-        SGMM_FT(t_);
-        fs_c[0] = t_ - fs_t0;
-        unsigned long long r1;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
-        if (lane == 0 && e < kStampWaves) {
-            for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
-            g_tstamps[e][7] = r1 - fs_r0;  // wall time in 10 ns ticks: the shader clock = [0] / [7]
-        }
-    }
-#undef SGMM_FT
-#endif
-#if defined(SGMM_STAMPS) && !defined(SGMM_STAMPS_PHASE)
-    {
-        unsigned long long t1;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
-        unsigned h_, x_;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(h_), "=s"(x_));
-        if (lane == 0 && e < kStampWaves) {
-            g_tstamps[e][0] = lite_t0;
-            g_tstamps[e][1] = t1;
-            g_tstamps[e][2] = lite_sl;
-            g_tstamps[e][3] = lite_ts;
-            g_tstamps[e][4] = lite_pk;
-            g_tstamps[e][5] = lite_pt;
-            g_thwid[e][0] = h_;
-            g_thwid[e][1] = x_;
-        }
-    }
-#endif
-    if (c < nch) {
-        // untracked start states keep the identity byte (never on the episode's path)
-        uint64_t cm = kIdentityMap;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s)
-            if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = (int64_t)e * kFrontierSlots + c;
-        cmaps[ci] = cm;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = cnt[s];
-        kinfo[ci] = (uint32_t)kc | (p0 << 29);
-    }
+    return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
 }
 
 // ------------------------------------------------------------------ exact ordered sum
@@ -1725,12 +1276,14 @@ __device__ __forceinline__ void store_record(double* fitness, int32_t* trades, i
 // stores, takes an arrival ticket (agent-scope atomic); the workgroup that
 // draws the last ticket reads every record with sc1 loads (ga_step_dev
 // <HANDOFF = true>) -- MI355X_MICROARCH.md inter-workgroup visibility, row 1
-// -- runs the GA step and resets the ticket for the next launch.
-__device__ void generation_tail(const StepArgs& sa0, const double* fitness0, const int32_t* trades0,
-                                unsigned char* lds, int* s_last) {
-    // this workgroup's population (one arrival ticket per population)
-    const int n_eps = sa0.pop_eps > 0 ? sa0.pop_eps : (int)gridDim.x;
-    const int k = sa0.pop_eps > 0 ? (int)blockIdx.x / sa0.pop_eps : 0;
+// -- runs the GA step and resets the ticket for the next launch.  e = the
+// episode whose record was stored (its population's ticket), n_total = the
+// launch's episodes (one population when pop_eps == 0).
+// The GA step of population k once all its records are stored (the last
+// arriver's part of generation_tail; the fused frontier launch's cleanup runs
+// it directly).
+__device__ void tail_run(const StepArgs& sa0, const double* fitness0, const int32_t* trades0, unsigned char* lds,
+                         int k, int n_eps) {
     StepArgs sa = sa0;
     sa.st = sa0.st + k;
     sa.master_mm = sa0.master_mm + (int64_t)k * sa0.n_mm;
@@ -1739,14 +1292,6 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
     if (sa0.history) sa.history = sa0.history + (int64_t)k * sa0.hist_cap;
     const double* fitness = fitness0 + (int64_t)k * n_eps;
     const int32_t* trades = trades0 + (int64_t)k * n_eps;
-    if (threadIdx.x == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int prev = __hip_atomic_fetch_add(&sa.st->arrivals, 1, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-        *s_last = prev == n_eps - 1;
-    }
-    __syncthreads();
-    if (!*s_last) return;
     if (sa0.seeds) sa.seed = sa0.seeds[k];
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: loads after the ticket
     SGMM_STAMP(blockIdx.x, 4);
@@ -1774,11 +1319,26 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
     SGMM_STAMP(blockIdx.x, 5);
 }
 
-// The validation launch's tail (StepArgs::mode 2): workgroup k holds the
+__device__ void generation_tail(const StepArgs& sa0, const double* fitness0, const int32_t* trades0,
+                                unsigned char* lds, int* s_last, int e, int n_total) {
+    // this episode's population (one arrival ticket per population)
+    const int n_eps = sa0.pop_eps > 0 ? sa0.pop_eps : n_total;
+    const int k = sa0.pop_eps > 0 ? e / sa0.pop_eps : 0;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(&sa0.st[k].arrivals, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = prev == n_eps - 1;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    tail_run(sa0, fitness0, trades0, lds, k, n_eps);
+}
+
+// The validation launch's tail (StepArgs::mode 2): episode k holds the
 // validation record (v, vtr: thread 0's values) of population k's post-tell
-// master and runs its bookkeeping -- no other workgroup's record is needed.
-__device__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag) {
-    const int k = blockIdx.x;
+// master and runs its bookkeeping -- no other episode's record is needed.
+__device__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag, int k) {
     __syncthreads();  // flag aliases LDS the caller has just read
     val_update_dev(sa.st + k, v, vtr, sa.master_mm + (int64_t)k * sa.n_mm,
                    sa.best_master ? sa.best_master + (int64_t)k * sa.n_mm : nullptr, sa.n_mm,
@@ -1786,35 +1346,44 @@ __device__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* 
 }
 
 // ------------------------------------------------------------------ path scan (no adversary)
-// One workgroup (16 waves) per episode, 4096-tick windows.
+// Per episode (one workgroup, or one wave of the fused frontier launch):
 //   1. wave 0: chunk start states from a wave-level scan of the chunk maps,
 //      and the episode's trades: each chunk's count along the path from its
 //      start state (8 bits per start state, written by the table);
 //   2. every thread: the rewards of its 4 ticks from the path plane of their
 //      chunk's start state (one coalesced row per chunk) -> LDS;
 //   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
-template <int NSM, int NT, bool FR, int TPB = NT>
-__global__ __launch_bounds__(TPB) void k_path_scan(
-    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
-    const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
-    const uint32_t* __restrict__ kinfo, const double* __restrict__ rew, double* __restrict__ fitness,
-    int32_t* __restrict__ trades_out, StepArgs step) {
-    // FR: the frontier kernel's chunks (frontier_len(T) ticks, at most 64 per
-    // episode, slots e * 64 + c, u32 trade counts, kinfo = merge tick | p0 << 29).
-    // TPB < NT: a TPB-thread workgroup with NT's window and block layout
-    // (TPB = 64, NT = 256: one wave -- the only one exact_sum_window<256> gives
-    // blocks to -- gathers 1024 values, so many more episodes run per CU)
+// FR: the frontier kernel's chunks (frontier_len(T, nw) ticks, at most 64 per
+// wave, slots e * 128 + c, u32 trade counts, kinfo = merge tick | p0 << 29).
+// TPB < NT: a TPB-thread workgroup with NT's window and block layout (TPB =
+// 64, NT = 256: one wave -- the only one exact_sum_window<256> gives blocks
+// to -- gathers 1024 values, so many more episodes run per CU).
+// SC1: the walk's outputs were handed over inside this launch (the fused
+// frontier kernel): every load of them is an sc1 load (ld_rec<true>).
+template <int NT>
+struct ScanShared {
+    double* sel;          // [NT * kSumTpt] the window (the last block padded in place)
+    SumLds<NT>* L;
+    uint8_t* start;       // chunk start states
+    uint32_t* kin;        // FR: the chunks' merge info
+    int* red;             // trades, then the tail's "last arriver" flag
+    unsigned char* tail;  // generation-tail scratch (aliases sel)
+};
+
+template <int NSM, int NT, bool FR, int TPB, bool SC1, bool TAIL = true>
+__device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, const sgmm_env_params* __restrict__ params,
+                                             int32_t inv_min, const uint64_t* __restrict__ cmaps,
+                                             const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ kinfo,
+                                             const double* __restrict__ rew, double* __restrict__ fitness,
+                                             int32_t* __restrict__ trades_out, const StepArgs& step, int n_total,
+                                             const ScanShared<NT>& sh) {
     static_assert(TPB == NT || (TPB == kWave && NT == 4 * kWave), "TPB = NT or one wave with NT = 256");
     constexpr int kWin = NT * kSumTpt;
-    extern __shared__ __align__(16) unsigned char lds[];
-    double* sel = reinterpret_cast<double*>(lds);  // [kWin]
-    __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[FR ? kFrontierSlots : kMaxLen / kChunk];
-    __shared__ uint32_t kin[FR ? kFrontierSlots : 1];
-    __shared__ int red_trades;
-    const int e = blockIdx.x;
+    double* sel = sh.sel;
+    uint8_t* start = sh.start;
+    uint32_t* kin = sh.kin;
     const int32_t T = ep.len[e];
-    const int CL = FR ? frontier_len(T, (int)ep.fnw[e]) : kChunk;
+    const int CL = FR ? frontier_len(T, nw) : kChunk;
     const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
     const int64_t cb = FR ? (int64_t)e * kFrontierSlots : (int64_t)chunk_base(so, e);
@@ -1825,7 +1394,7 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
         int tr = 0;
         for (int c0 = 0; c0 < nch; c0 += kWave) {
             const int c = c0 + lane;
-            const uint64_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
+            const uint64_t m = c < nch ? ld_rec<SC1>(cmaps + cb + c) : kIdentityMap;
             const uint64_t k = (!FR && c < nch) ? ctr[cb + c] : 0;
             const uint64_t inc = wave_map_scan(m);
             uint64_t excl = shfl_up_u64(inc, 1);
@@ -1834,8 +1403,8 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
             if (c < nch) start[c] = (uint8_t)st;
             if (FR) {
                 if (c < nch) {
-                    tr += (int)reinterpret_cast<const uint32_t*>(ctr)[(cb + c) * 8 + st];
-                    kin[c] = kinfo[cb + c];
+                    tr += (int)ld_rec<SC1>(reinterpret_cast<const uint32_t*>(ctr) + (cb + c) * 8 + st);
+                    kin[c] = ld_rec<SC1>(kinfo + cb + c);
                 }
             } else {
                 tr += (int)((k >> (8 * st)) & 0xFFu);
@@ -1844,7 +1413,7 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
         }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, kWave);
-        if (lane == 0) red_trades = tr;
+        if (lane == 0) *sh.red = tr;
     }
     __syncthreads();
     SGMM_STAMP(e, 1);
@@ -1877,7 +1446,8 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
 #pragma unroll
                     for (int j = 0; j < kSumTpt; ++j) {
                         const int jj = min(j, n - 1 - i0);
-                        r[g][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
+                        r[g][j] = ld_rec<SC1>(rew + (u + jj >= kc ? pp0 : pst) * ep.rs + rb +
+                                              (int64_t)(u + jj) * kFrontierLanes);
                     }
                 } else {
                     const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
@@ -1907,7 +1477,7 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
         sw_g += sw_b - sw_a;
 #endif
         if (w0 + kWin < T) gather(w0 + kWin);  // in flight during the sum
-        S = exact_sum_window<NT>(sel, n, S, L);
+        S = exact_sum_window<NT>(sel, n, S, *sh.L);
 #ifdef SGMM_STAMPS
         SGMM_SW(sw_a);
         sw_s += sw_a - sw_b;
@@ -1926,13 +1496,749 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     int tr = 0;  // thread 0's record (the tails read it there only)
     double total = S;
     if (tid == 0) {
-        tr = red_trades;
+        tr = *sh.red;
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
         store_record(fitness, trades_out, e, total, tr);
     }
-    if (step.st) {
-        if (step.mode == 2) validation_tail(step, total, tr, &red_trades);
-        else generation_tail(step, fitness, trades_out, lds, &red_trades);
+    if (TAIL && step.st) {
+        if (step.mode == 2) validation_tail(step, total, tr, sh.red, e);
+        else generation_tail(step, fitness, trades_out, sh.tail, sh.red, e, n_total);
+    }
+}
+
+// one workgroup per episode (the table path, and the frontier path unfused)
+template <int NSM, int NT, bool FR, int TPB = NT>
+__global__ __launch_bounds__(TPB) void k_path_scan(
+    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
+    const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
+    const uint32_t* __restrict__ kinfo, const double* __restrict__ rew, double* __restrict__ fitness,
+    int32_t* __restrict__ trades_out, StepArgs step) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    __shared__ SumLds<NT> L;
+    __shared__ uint8_t start[FR ? kFrontierSlots : kMaxLen / kChunk];
+    __shared__ uint32_t kin[FR ? kFrontierSlots : 1];
+    __shared__ int red_trades;
+    const int e = blockIdx.x;
+    const ScanShared<NT> sh{reinterpret_cast<double*>(lds), &L, start, kin, &red_trades, lds};
+    scan_episode<NSM, NT, FR, TPB, false>(e, FR ? (int)ep.fnw[e] : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew,
+                                          fitness, trades_out, step, (int)gridDim.x, sh);
+}
+
+// ------------------------------------------------------------------ frontier kernel (the walk)
+// The fused launch (FUSED): walks and path scans in one kernel.  Blocks
+// [0, nwalk) walk one episode each; when a walk ends, its wave publishes the
+// episode on its XCD's queue (its stores drained, then one lane's agent-scope
+// atomics) and leaves.  Blocks [nwalk, nwalk + nscan) are scanners: each
+// claims episodes from its own XCD's queue and scans them as they arrive, so
+// the scans run in the walks' tail instead of after it.  A scanner waits (with
+// s_sleep) only once every walk has started -- then every pending entry is
+// sure to come -- and otherwise gives up after a bounded wait and leaves; the
+// cleanup launch after the kernel scans whatever is left, so no dispatch order
+// can deadlock the launch.  Producer and consumer share the XCD's L2, so the
+// walk's outputs are plain stores (write-back, whole lines; write-through
+// stores of the 8-byte plane rows were ~100x slower) and the scan reads them
+// with sc1 loads past its own L1; episodes' output blocks never share a line
+// (frontier_base), and a split episode (two waves, maybe on two XCDs) is never
+// fused.
+struct FrontierQueue {
+    uint32_t* ctl;     // per XCD x: ctl[32 x] head (next entry to claim), u64 at ctl + 32 x + 2:
+                       // tail (next free slot) | done << 32 (set once every walk has pushed);
+                       // ctl[32 kXcds] walks started, ctl[32 kXcds + 32] walks finished,
+                       // ctl[32 kXcds + 64] episodes scanned
+    uint32_t* q;       // per XCD x: q[x * n + i] = episode + 1; 0 = not yet stored
+    double* fitness;
+    int32_t* trades;
+    StepArgs step;
+    int32_t n;         // episodes of the launch
+    int32_t nwalk;     // walk blocks (the scanners follow)
+    int32_t poll;      // s_sleep(127) rounds between two polls of an empty queue
+};
+constexpr int kXcds = 8;
+constexpr int kScanPatience = 2048;  // idle polls a scanner waits for walks still to start
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return x & (kXcds - 1);
+}
+constexpr int kFusedScanNT = 4 * kWave;                             // one-wave scans: 256-thread window layout
+constexpr int kFusedSel = kFusedScanNT * kSumTpt * (int)sizeof(double);  // 8 KB window
+constexpr int kFusedScanLds = kFusedSel + (int)sizeof(SumLds<kFusedScanNT>) + kFrontierSlots +
+                              4 * kFrontierSlots + 16;
+static_assert(sizeof(SumLds<kFusedScanNT>) % 8 == 0, "scan LDS carve-out alignment");
+
+template <class T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
+    typedef __attribute__((address_space(1))) T gT;
+    __hip_atomic_store((gT*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool SC1, class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+    if constexpr (SC1) st_sc1(p, v);
+    else *p = v;
+}
+__device__ __forceinline__ uint32_t atomic_peek(uint32_t* p) {  // coherent read (an agent-scope RMW)
+    return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t atomic_peek64(uint64_t* p) {
+    return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t* queue_state(const FrontierQueue& fq, uint32_t x) {
+    return reinterpret_cast<uint64_t*>(fq.ctl + 32 * x + 2);
+}
+
+typedef __attribute__((address_space(3))) unsigned char lds_u8;
+
+// The scans of the fused launch, a separate (not inlined) function: its
+// registers are allocated apart from the walk's, so the walk keeps its three
+// waves per SIMD.  `lds` is the wave's LDS block (the walk's, dead by now).
+// A scanner (or, CLEANUP, a block of the cleanup launch, which sweeps every
+// XCD's queue after the fused kernel has ended).
+template <int NSI, bool CLEANUP>
+__device__ __forceinline__ void fused_scans(const EpArrays ep, const sgmm_env_params* __restrict__ params,
+                                            int32_t inv_min, const uint64_t* __restrict__ cmaps,
+                                            const uint32_t* __restrict__ ctr32, const uint32_t* __restrict__ kinfo,
+                                            const double* __restrict__ rew, const FrontierQueue fq, lds_u8* lds) {
+    using SL = SumLds<kFusedScanNT>;
+    typedef __attribute__((address_space(3))) double lds_f64;
+    typedef __attribute__((address_space(3))) SL lds_sl;
+    typedef __attribute__((address_space(3))) uint32_t lds_u32;
+    typedef __attribute__((address_space(3))) int lds_i32;
+    const ScanShared<kFusedScanNT> sh{(double*)(lds_f64*)lds, (SL*)(lds_sl*)(lds + kFusedSel),
+                                      (uint8_t*)(lds + kFusedSel + sizeof(SL)),
+                                      (uint32_t*)(lds_u32*)(lds + kFusedSel + sizeof(SL) + kFrontierSlots),
+                                      (int*)(lds_i32*)(lds + kFusedSel + sizeof(SL) + 5 * kFrontierSlots),
+                                      (unsigned char*)lds};
+    const int lane = threadIdx.x;
+    uint32_t* started = fq.ctl + 32 * kXcds;
+    uint32_t x = CLEANUP ? 0u : xcc_id();
+    int patience = 0;
+#ifdef SGMM_STAMPS
+    // scanner timeline (row 32768 + scanner): start, first claim, end (realtime),
+    // scans, idle polls, XCC, time spent in scans (realtime ticks)
+    unsigned long long sc_t0, sc_first = 0, sc_n = 0, sc_polls = 0, sc_busy = 0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_t0)::"memory");
+    const int sc_row = 32768 + (CLEANUP ? 16384 + (int)blockIdx.x : (int)blockIdx.x - fq.nwalk);
+#endif
+    while (true) {
+        // 0..: an entry of queue x claimed; -1: queue x empty and no more will
+        // come (or this scanner gives up); -2: empty for now.  An idle poll is
+        // ONE atomic on the XCD's state word (pollers of one word saturate it)
+        int32_t h = -1;
+        if (lane == 0) {
+            uint32_t* head = fq.ctl + 32 * x;
+            const uint64_t sw = CLEANUP ? (1ull << 32) | atomic_peek(reinterpret_cast<uint32_t*>(queue_state(fq, x)))
+                                        : atomic_peek64(queue_state(fq, x));
+            const uint32_t tail = (uint32_t)sw;
+            const bool done = (sw >> 32) != 0;
+            h = done ? -1 : -2;
+            uint32_t cur = atomic_peek(head);
+            while (cur < tail) {  // claim entry cur
+                if (__hip_atomic_compare_exchange_strong(head, &cur, cur + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)) {
+                    h = (int32_t)cur;
+                    break;
+                }
+            }
+            if (!CLEANUP && h == -2 && (++patience & 63) == 0 && atomic_peek(started) < (uint32_t)fq.nwalk &&
+                patience > kScanPatience)
+                h = -1;  // walks still to start: leave the slot to them (the cleanup launch finishes up)
+        }
+        h = __builtin_amdgcn_readfirstlane(h);
+        if (h == -1) {
+            if (!CLEANUP || ++x == (uint32_t)kXcds) break;
+            continue;
+        }
+        if (h == -2) {
+#ifdef SGMM_STAMPS
+            ++sc_polls;
+#endif
+            for (int i = 0; i < fq.poll; ++i) __builtin_amdgcn_s_sleep(127);
+            continue;
+        }
+        uint32_t ent = 0;
+        if (lane == 0) {  // its pusher has taken the slot and is about to store it
+            uint32_t* q = fq.q + (int64_t)x * fq.n;
+            while ((ent = atomic_peek(&q[h])) == 0u) __builtin_amdgcn_s_sleep(1);
+        }
+        ent = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent);
+#ifdef SGMM_STAMPS
+        unsigned long long sc_a;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_a)::"memory");
+        if (!sc_first) sc_first = sc_a;
+        ++sc_n;
+#endif
+        scan_episode<NSI, kFusedScanNT, true, kWave, true, false>(
+            (int)ent - 1, 1, ep, params, inv_min, cmaps, reinterpret_cast<const uint64_t*>(ctr32), kinfo, rew,
+            fq.fitness, fq.trades, fq.step, fq.n, sh);
+        if (lane == 0) {  // its record stored (sc1) and drained: one more episode scanned
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(fq.ctl + 32 * (kXcds + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#ifdef SGMM_STAMPS
+        {
+            unsigned long long sc_b;
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_b)::"memory");
+            sc_busy += sc_b - sc_a;
+        }
+#endif
+        __syncthreads();  // the LDS carve-out is reused by the next scan
+    }
+#ifdef SGMM_STAMPS
+    {
+        unsigned long long sc_t1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_t1)::"memory");
+        if (lane == 0 && sc_row < kStampWaves) {
+            g_tstamps[sc_row][0] = sc_t0;
+            g_tstamps[sc_row][1] = sc_first;
+            g_tstamps[sc_row][2] = sc_t1;
+            g_tstamps[sc_row][3] = sc_n;
+            g_tstamps[sc_row][4] = sc_polls;
+            g_tstamps[sc_row][5] = x;
+            g_tstamps[sc_row][6] = sc_busy;
+        }
+    }
+#endif
+}
+
+template <int H, int NSI, bool FUSED>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(
+    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
+    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ cmaps, uint32_t* __restrict__ ctr32,
+    uint32_t* __restrict__ kinfo, double* __restrict__ rew, FrontierQueue fq) {
+    static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16, KS = H / 4;
+    constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
+    // LDS (~13 KB per wave, so 3 waves per SIMD fit): the genome is staged in
+    // `big`, the weights the loop needs are copied out, then `big` holds the
+    // half-activation transpose buffer and the per-state rewards; a scanner
+    // (FUSED) holds its window, records and chunk tables there
+    constexpr int kWalkBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
+    constexpr int kBig = (FUSED && kFusedScanLds > kWalkBig) ? kFusedScanLds : kWalkBig;
+    __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
+    if constexpr (FUSED) {
+        if ((int)blockIdx.x >= fq.nwalk) {  // a scanner
+            fused_scans<NSI, false>(ep, params, inv_min, cmaps, ctr32, kinfo, rew, fq, (lds_u8*)big);
+            return;
+        }
+        if (threadIdx.x == 0)
+            __hip_atomic_fetch_add(fq.ctl + 32 * kXcds, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // wave b: the whole episode at order position b (b < fwhole), else chunk
+    // group g of a split episode (two waves each, longest episodes first)
+    const int b = (int)blockIdx.x;
+    const int pos = b < ep.fwhole ? b : ep.fwhole + ((b - ep.fwhole) >> 1);
+    const int nw = b < ep.fwhole ? 1 : 2, cg = b < ep.fwhole ? 0 : (b - ep.fwhole) & 1;
+    const int e = ep.order ? ep.order[pos] : pos;
+    if (!FUSED && cg == 0 && threadIdx.x == 0) ep.fnw[e] = (uint32_t)nw;  // fused: the queue entry carries it
+    const int32_t T = ep.len[e];
+
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 4];  // (W3[0][j], W3[1][j]) pairs, then b3
+    __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
+    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
+    __shared__ __attribute__((aligned(16))) float b2s[H];
+    // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
+    // successor (bits 9-11) and the fill (bit 12) written back by the column
+    __shared__ uint16_t pl[kWave * (NSI - 1)];
+
+    auto walk = [&]() {  // the episode's walk (returns early past its last chunk)
+    if (T <= 0) return;  // block-uniform
+    const int CL = frontier_len(T, nw);
+    const int nch = (T + CL - 1) / CL;
+    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
+    const int lane = threadIdx.x, grp = lane >> 4, col = lane & 15;
+    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
+    const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
+    const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int t0 = c * CL;
+    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
+
+    float* gsm = reinterpret_cast<float*>(big);
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __syncthreads();
+    if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
+    if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
+    if (lane < H) {
+        w1x[lane & 3][lane >> 2] = gsm[L::W1 + 3 * lane + 2];
+        l1w[lane][0] = gsm[L::W1 + 3 * lane];
+        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
+        l1w[lane][2] = gsm[L::B1 + lane];
+        l1w[lane][3] = gsm[L::W1 + 3 * lane + 2];
+        b2s[lane] = gsm[L::B2 + lane];
+    }
+    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+    __syncthreads();  // gsm is dead from here: big becomes hb + rl
+    float* hb = reinterpret_cast<float*>(big);                          // [64][HP]
+    double* rl = reinterpret_cast<double*>(big + kWave * HP * 4);       // [NSI][64]
+    const sgmm_env_params p = params[ep.param[e]];
+
+    // per-lane path bookkeeping: byte s of cur = the state of the path that
+    // started the chunk in state s (tracked starts: bits of sset)
+    const uint32_t all = (1u << nsi) - 1u;
+    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
+    uint64_t cur = kIdentityMap;
+    // trade count along the path from each tracked start: 16 bits per start,
+    // two per word (a chunk has < 2^16 ticks: kFrontierMaxLen)
+    uint32_t cnt[(NSI + 1) / 2];
+#pragma unroll
+    for (int s = 0; s < (NSI + 1) / 2; ++s) cnt[s] = 0;
+    bool merged = __builtin_popcount(sset) <= 1;
+    int kc = merged ? 0 : CL;
+    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
+#ifdef SGMM_STAMPS
+    // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
+    // slots and tile-slots run (slots 2, 3); nothing inside the loop waits
+    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_pk = 0, lite_pt = 0, lite_s8 = 0, lite_s16 = 0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
+#endif
+#ifdef SGMM_STAMPS_PHASE
+    // per wave (episode): 0 cycles, 1 layers 1-2 (MFMA issue), 2 relu + transpose
+    // (MFMA drain), 3 layer 3, 4 FPT step, 5 per-tick head (frontier, signals,
+    // layer-1 terms), 6 planes, 7 wall time (10 ns ticks)
+    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
+#define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
+    SGMM_FT(fs_t0);
+#endif
+    int64_t ti = tick_of(0);
+    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
+#pragma unroll 1
+    for (int tt = 0; tt < CL; ++tt) {
+#ifdef SGMM_STAMPS_PHASE
+        SGMM_FT(fs_a);
+#endif
+        const bool act = tt < ntl;
+        const float s1 = ns1, s2 = ns2;
+        // this tick's prices: first used after the tick's MLP, which hides the load
+        const double tmid = tk.mid_next[ti], task = tk.best_ask[ti], tbid = tk.best_bid[ti];
+        const double tbmax = tk.buy_max[ti], tsmin = tk.sell_min[ti];
+        ti = tick_of(tt + 1);
+        ns1 = tk.s1n[ti];
+        ns2 = tk.s2n[ti];
+        // frontier: the distinct current states of the tracked paths
+        uint32_t fmask = 0;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s)
+            if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
+        if (!act) fmask = 0;
+#ifdef SGMM_STAMPS
+        {
+            // what (chunk, state) pairs packed densely into the 64 columns would need
+            int so = __builtin_popcount(fmask);
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) so += __shfl_xor(so, m, kWave);
+            lite_pk += (so + 63) / 64;
+            lite_pt += (so + 15) / 16;
+        }
+#endif
+        // the weights stay in LDS: an opaque base per tick keeps the compiler
+        // from hoisting ~90 loop-invariant weight loads into registers
+        lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
+        asm volatile("" : "+v"(l1p));
+        // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
+        float pre[4][KS];
+        // the frontier of each B-operand sample's chunk (lane 16q + col): the
+        // slots take their k-th state from it, no per-slot permute
+        uint32_t remq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) remq[q] = (uint32_t)__shfl((int)fmask, 16 * q + col, kWave);
+        {
+            float xs0[4], xs1[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                xs0[q] = __shfl(s1, 16 * q + col, kWave);
+                xs1[q] = __shfl(s2, 16 * q + col, kWave);
+            }
+#pragma unroll
+            for (int i = 0; i < KS; ++i) {
+                const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
+#pragma unroll
+                for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
+            }
+        }
+#ifdef SGMM_STAMPS_PHASE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        SGMM_FT(fs_b);
+        fs_c[5] += fs_b - fs_a;
+#endif
+        uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
+        uint32_t trm = 0;                 // bit f: a fill from frontier state f
+        // Slot 0: each lane's first frontier state in its own column (the
+        // common case: most ticks have one state per chunk).  Slots 1..: the
+        // remaining (chunk, state) pairs packed densely into the 64 columns --
+        // a chunk whose paths stay apart costs its extra states, not extra
+        // slots for the whole wave.  Each column computes with its pair's own
+        // inputs (the chunk's signals and prices, the state's inventory), so
+        // every (tick, state) result is bit-identical to the unpacked walk.
+        const uint32_t ext = fmask & (fmask - 1u);  // frontier states after the first
+        const uint32_t nex = (uint32_t)__builtin_popcount(ext);
+        const uint64_t eb0 = __ballot(nex & 1u), eb1 = __ballot(nex & 2u), eb2 = __ballot(nex & 4u);
+        const int epfx = mbcnt64(eb0) + 2 * mbcnt64(eb1) + 4 * mbcnt64(eb2);  // first pair of this lane
+        const int etot = __popcll(eb0) + 2 * __popcll(eb1) + 4 * __popcll(eb2);  // extra pairs (uniform)
+        {
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    pl[pp++] = (uint16_t)((lane << 3) | __builtin_ctz(r));
+                    r &= r - 1u;
+                }
+        }
+        const bool any0 = __ballot(fmask != 0u) != 0ull;
+        const int nx = (etot + kWave - 1) / kWave;
+#ifdef SGMM_STAMPS
+        lite_sl += (any0 ? 1 : 0) + nx;
+        if (tt == 7) lite_s8 = lite_sl;    // slots run in the first 8 / 16 ticks (heaviness probes)
+        if (tt == 15) lite_s16 = lite_sl;
+        lite_ts += (any0 ? 4 : 0) + (etot + 15) / 16;
+#endif
+        // layers 1-3 of the four 16-column tiles' samples (tiles >= NQ skipped):
+        // x2q / pq = inv / 2 and the layer-1 signal terms of sample 16q + col
+        auto mlp = [&](auto nq, const float(&x2q)[4], const float(&pq)[4][KS], float& o0, float& o1) {
+            constexpr int NQ = decltype(nq)::value;
+            lds_cf* w3p = (lds_cf*)(&w3i[0]);
+            asm volatile("" : "+v"(w3p));
+            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
+            asm volatile("" : "+v"(w1p));
+            lds_cf* b2p = (lds_cf*)(&b2s[0]);
+            asm volatile("" : "+v"(b2p));
+            // layer 1 + layer 2: 4 x NT independent accumulator chains issued
+            // k-step by k-step keep the matrix pipe busy
+            f32x4 acc[4][NT];
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) {
+                const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) acc[q][rt] = bb;
+            }
+#pragma unroll
+            for (int i4 = 0; i4 < KS; i4 += 4) {
+                const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int q = 0; q < NQ; ++q) {
+                        const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pq[q][i4 + r]));
+#pragma unroll
+                        for (int rt = 0; rt < NT; ++rt)
+                            acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
+                    }
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                SGMM_FT(t_);  // MFMAs issued (not completed)
+                fs_c[1] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+#pragma unroll
+                for (int rt = 0; rt < NT; ++rt) {
+                    f32x4 v;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+                }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[2] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+            // layer 3 of this lane's column, in neuron order (the canonical chain)
+            o0 = w3p[2 * H];
+            o1 = w3p[2 * H + 1];
+#pragma unroll 1
+            for (int j8 = 0; j8 < H / 8; ++j8) {
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int j4 = 2 * j8 + jj;
+                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+                    for (int r2 = 0; r2 < 2; ++r2) {
+                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
+                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                    }
+                }
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[3] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        };
+        if (any0) {
+            float x2q[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
+                x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
+            }
+            float o0, o1;
+            mlp(IntC<4>{}, x2q, pre, o0, o1);
+            const bool has = fmask != 0u;
+            const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
+            if (has) {
+                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
+                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
+                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
+                rl[f * kWave + lane] = so1.reward;
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[4] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        }
+#pragma unroll 1
+        for (int x = 0; x < nx; ++x) {
+            // column lane = pair 64 x + lane: (chunk lane src, state f)
+            const int pidx = kWave * x + lane;
+            const bool has = pidx < etot;
+            const uint32_t v = has ? (uint32_t)pl[pidx] : 0u;
+            const int src = (int)(v >> 3);
+            const uint32_t f = v & 7u;
+            float x2q[4], pq[4][KS];
+            {
+                float xs0[4], xs1[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t vq = (uint32_t)__shfl((int)v, 16 * q + col, kWave);
+                    const int sq = (int)(vq >> 3);
+                    x2q[q] = (float)(inv_min + (int)(vq & 7u)) * 0.5f;
+                    xs0[q] = __shfl(s1, sq, kWave);
+                    xs1[q] = __shfl(s2, sq, kWave);
+                }
+                lds_cf* l1q = (lds_cf*)(&l1w[0][0]);
+                asm volatile("" : "+v"(l1q));
+#pragma unroll
+                for (int i = 0; i < KS; ++i) {
+                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1q + 4 * (4 * i + grp));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) pq[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
+                }
+            }
+            const int ntile = min(4, (etot - kWave * x + 15) >> 4);
+            float o0, o1;
+            if (ntile == 1)
+                mlp(IntC<1>{}, x2q, pq, o0, o1);
+            else if (ntile == 2)
+                mlp(IntC<2>{}, x2q, pq, o0, o1);
+            else
+                mlp(IntC<4>{}, x2q, pq, o0, o1);
+            // the FPT step with the pair's chunk's prices
+            const double smid = __shfl(tmid, src, kWave), sask = __shfl(task, src, kWave);
+            const double sbid = __shfl(tbid, src, kWave), sbmax = __shfl(tbmax, src, kWave);
+            const double ssmin = __shfl(tsmin, src, kWave);
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, smid, sask, sbid, sbmax, ssmin);
+            if (has) {
+                rl[f * kWave + src] = so1.reward;
+                const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
+                pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
+            }
+#ifdef SGMM_STAMPS_PHASE
+            {
+                unsigned long long t_;
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                SGMM_FT(t_);
+                fs_c[4] += t_ - fs_b;
+                fs_b = t_;
+            }
+#endif
+        }
+        {
+            // the owner lane collects its extra states' successors and fills
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    const uint32_t f = (uint32_t)__builtin_ctz(r);
+                    r &= r - 1u;
+                    const uint32_t w = pl[pp++];
+                    stepmap = (stepmap & ~(0xFFull << (8 * f))) | ((uint64_t)((w >> 9) & 7u) << (8 * f));
+                    trm |= ((w >> 12) & 1u) << f;
+                }
+        }
+#ifdef SGMM_STAMPS_PHASE
+        SGMM_FT(fs_b);
+#endif
+        // the tick's rewards along the tracked paths; once they have merged only plane p0
+        if (act) {
+            // planes in tick-offset-major order (row u of an episode's block holds
+            // the 64 chunks' rewards at offset u): one coalesced 512-byte store
+            // per plane and tick; row-major rows made every 8-byte store a
+            // partial line and the L2 wrote ~6x the bytes back
+            // plane s's row: one per-lane base plus a uniform offset (the plane
+            // stride made opaque per tick, so the compiler keeps one 64-bit
+            // address, not one per plane: that saved the registers of four)
+            int64_t prs = ep.rs;
+            asm volatile("" : "+s"(prs));
+            // uniform: the group's first row (readfirstlane: e came from a load)
+            const uint64_t pa = reinterpret_cast<uint64_t>(rew + rbase);
+            uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa);
+            asm volatile("" : "+s"(pu));
+            double* const prow = reinterpret_cast<double*>(pu);
+            const int64_t toff = (int64_t)tt * kFrontierLanes;
+#pragma unroll
+            for (int s = 0; s < NSI; ++s) {
+                if (!((sset >> s) & 1u)) continue;
+                const uint32_t st = map_get(cur, (uint32_t)s);
+                if (!merged || (uint32_t)s == p0) prow[s * prs + toff + lane] = rl[st * kWave + lane];
+                cnt[s >> 1] += ((trm >> st) & 1u) << (16 * (s & 1));
+            }
+            cur = map_then(cur, stepmap);
+            if (!merged) {
+                uint32_t fm = 0;
+#pragma unroll
+                for (int s = 0; s < NSI; ++s)
+                    if ((sset >> s) & 1u) fm |= 1u << map_get(cur, (uint32_t)s);
+                if (__builtin_popcount(fm) <= 1) {
+                    merged = true;
+                    kc = tt + 1;
+                }
+            }
+        }
+#ifdef SGMM_STAMPS_PHASE
+        {
+            unsigned long long t_;
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            SGMM_FT(t_);
+            fs_c[6] += t_ - fs_b;
+        }
+#endif
+    }
+#ifdef SGMM_STAMPS_PHASE
+    {
+        unsigned long long t_;
+        SGMM_FT(t_);
+        fs_c[0] = t_ - fs_t0;
+        unsigned long long r1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+        if (lane == 0 && e < kStampWaves) {
+            for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
+            g_tstamps[e][7] = r1 - fs_r0;  // wall time in 10 ns ticks: the shader clock = [0] / [7]
+        }
+    }
+#undef SGMM_FT
+#endif
+#if defined(SGMM_STAMPS) && !defined(SGMM_STAMPS_PHASE)
+    {
+        unsigned long long t1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        unsigned h_, x_;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(h_), "=s"(x_));
+        const int srow = e + cg * 16384;  // a split episode's second group: row e + 16384
+        if (lane == 0 && srow < 32768) {
+            g_tstamps[srow][0] = lite_t0;
+            g_tstamps[srow][1] = t1;
+            g_tstamps[srow][2] = lite_sl;
+            g_tstamps[srow][3] = lite_ts;
+            g_tstamps[srow][4] = lite_pk;
+            g_tstamps[srow][5] = lite_pt;
+            g_tstamps[srow][6] = lite_s8;
+            g_tstamps[srow][7] = lite_s16;
+            g_thwid[srow][0] = h_;
+            g_thwid[srow][1] = x_;
+        }
+    }
+#endif
+    if (c < nch) {
+        // untracked start states keep the identity byte (never on the episode's path)
+        uint64_t cm = kIdentityMap;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s)
+            if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
+        const int64_t ci = (int64_t)e * kFrontierSlots + c;
+        cmaps[ci] = cm;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+        kinfo[ci] = (uint32_t)kc | (p0 << 29);
+    }
+    };
+    walk();
+    if constexpr (FUSED) {
+        const int lane = threadIdx.x;
+        // publish on this XCD's queue: the wave's stores drained into the L2,
+        // then one lane's atomics (every episode is one wave here); the push
+        // completes before the walk counts as finished
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            const uint32_t x = xcc_id();
+            const uint32_t slot = (uint32_t)__hip_atomic_fetch_add(queue_state(fq, x), (uint64_t)1, __ATOMIC_RELAXED,
+                                                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_exchange(&fq.q[(int64_t)x * fq.n + slot], (uint32_t)(e + 1), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint32_t fin = __hip_atomic_fetch_add(fq.ctl + 32 * kXcds + 32, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            if (fin + 1 == (uint32_t)fq.nwalk)  // the last walk: every push is done, tell the scanners
+                for (uint32_t y = 0; y < (uint32_t)kXcds; ++y)
+                    __hip_atomic_fetch_add(queue_state(fq, y), 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// After the fused launch: scans any episode its scanners left (normally
+// none), then -- every episode scanned -- runs each population's GA tail
+// (the tell, or the validation bookkeeping of mode 2): block k takes
+// population k.  The scanners carry no tail code: it would not fit their
+// registers beside the walk's.
+template <int NSI>
+__global__ __launch_bounds__(kWave) void k_frontier_cleanup(EpArrays ep, const sgmm_env_params* __restrict__ params,
+                                                             int32_t inv_min, const uint64_t* __restrict__ cmaps,
+                                                             const uint32_t* __restrict__ ctr32,
+                                                             const uint32_t* __restrict__ kinfo,
+                                                             const double* __restrict__ rew, FrontierQueue fq) {
+    __shared__ __attribute__((aligned(16))) unsigned char big[kFusedScanLds];
+    fused_scans<NSI, true>(ep, params, inv_min, cmaps, ctr32, kinfo, rew, fq, (lds_u8*)big);
+    const StepArgs& sa = fq.step;
+    if (!sa.st) return;
+    const int n_eps = sa.pop_eps > 0 ? sa.pop_eps : fq.n;
+    const int K = fq.n / n_eps;
+    if ((int)blockIdx.x >= K) return;
+    if (threadIdx.x == 0) {  // the leftovers are scanned by blocks of this launch, all resident
+        while (atomic_peek(fq.ctl + 32 * (kXcds + 2)) < (uint32_t)fq.n) __builtin_amdgcn_s_sleep(8);
+    }
+    __syncthreads();
+    __shared__ int flag;
+    for (int k = blockIdx.x; k < K; k += gridDim.x) {
+        if (sa.mode == 2) {  // one validation episode per population: episode k
+            const double v = ld_rec<true>(fq.fitness + k);
+            const int32_t vtr = ld_rec<true>(fq.trades + k);
+            validation_tail(sa, v, vtr, &flag, k);
+        } else {
+            tail_run(sa, fq.fitness, fq.trades, big, k, n_eps);
+        }
+        __syncthreads();
     }
 }
 
@@ -2039,7 +2345,7 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;
         store_record(fitness, trades_out, e, total, tr);
     }
-    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades);
+    if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades, e, (int)gridDim.x);
 }
 
 // ------------------------------------------------------------------ direct (trace) path
@@ -2232,8 +2538,8 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     return SGMM_OK;
 }
 
-// plane stride: every tick plus the frontier layout's 512 padding slots per episode
-static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + 4 * kFrontierSlots * n + 31) & ~int64_t(31); }
+// plane stride: every tick plus the frontier layout's 528 padding rows per episode
+static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + kFrontierPad * n + 31) & ~int64_t(31); }
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
@@ -2288,7 +2594,12 @@ static size_t ws_cmaps(int32_t n, int64_t steps) {
 static size_t ws_ctr(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps) * sizeof(uint64_t), n_frontier_slots(n) * 8 * sizeof(uint32_t)));
 }
-static size_t ws_kinfo(int32_t n) { return align256((n_frontier_slots(n) + n) * sizeof(uint32_t)); }
+// u32 kinfo[n * 128] | u32 waves[n] | (256-aligned) the fused launch's queues:
+// u32 ctl[11][32] (head, tail per XCD; walks started; walks finished;
+// episodes scanned), u32 q[8][n] -- zeroed by the launch
+static size_t ws_kinfo_head(int32_t n) { return align256((n_frontier_slots(n) + n) * sizeof(uint32_t)); }
+static size_t ws_queue(int32_t n) { return 4 * 32 * (kXcds + 3) + (size_t)4 * kXcds * n; }
+static size_t ws_kinfo(int32_t n) { return ws_kinfo_head(n) + align256(ws_queue(n)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 // The workspace of a batch with n_inventory inventory values, with or
@@ -2353,6 +2664,15 @@ static int simd_count() {
         n = 4 * cus;
     }
     return n;
+}
+// SGMM_FRONTIER_FUSED=1: the frontier kernel scans finished episodes itself
+// (FrontierQueue scanners + the cleanup launch) instead of the separate
+// one-wave path-scan launch.  Off by default: measured slower on config 3
+// (783 vs 734 us per generation) -- scans beside the
+// walks' tail slow those walks, and the last walks' scans still follow them.
+static bool frontier_fused() {
+    const char* v = std::getenv("SGMM_FRONTIER_FUSED");
+    return v && std::strcmp(v, "1") == 0;
 }
 static int32_t frontier_whole(int32_t n) {
     const char* v = std::getenv("SGMM_FRONTIER_NW");
@@ -2500,12 +2820,41 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
+    SGMM_REQUIRE(!fr || eps->max_len <= kFrontierMaxLen, "max_len=%d > %lld ticks per episode",
+                 eps->max_len, (long long)kFrontierMaxLen);
+    // the fused launch: walks and scans in one kernel (the GA tail included);
+    // its scratch for the tail must fit the 8 KB scan window it aliases
+    // (split episodes' two waves may run on two XCDs: never fused)
+    const bool fused = fr && eps->max_len > 0 && frontier_fused() && ep.fwhole == eps->n &&
+                       (!step.st || step_lds_bytes(kWave, step) <= (size_t)kFusedSel);
     if (fr && eps->max_len > 0) {
-        ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
-        const dim3 grid(ep.fwhole + 2 * (eps->n - ep.fwhole)), block(kWave);
-#define SGMM_FRONTIER(H_, NSI_)                                                                            \
-    SGMM_LAUNCH((k_policy_frontier<H_, NSI_>), grid, block, 0, s, *ticks, ep, params, src, eps->inv_min, nsi, \
-                cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew)
+        ProfScope prof(fused ? (vt ? "val_policy_frontier_scan" : "policy_frontier_scan")
+                             : (vt ? "val_policy_frontier" : "policy_frontier"), s);
+        const int nwalk = ep.fwhole + 2 * (eps->n - ep.fwhole);
+        // scanners: the wave slots the walks leave free (3 waves per SIMD), at
+        // least 128 and at most one per episode
+        int nscan = fused ? std::min(eps->n, std::max(128, std::min(1024, 3 * simd_count() - nwalk))) : 0;
+        if (const char* v = std::getenv("SGMM_SCANNERS"); fused && v && std::atoi(v) > 0)
+            nscan = std::min(eps->n, std::atoi(v));
+        const char* pv = std::getenv("SGMM_SCAN_POLL");
+        const int poll = pv && std::atoi(pv) > 0 ? std::atoi(pv) : 1;
+
+        const dim3 grid(nwalk + nscan), block(kWave);
+        FrontierQueue fq{};
+        if (fused) {
+            uint32_t* ctl = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(kinfo) + ws_kinfo_head(eps->n));
+            fq = FrontierQueue{ctl, ctl + 32 * (kXcds + 3), fitness, trades, step, eps->n, nwalk, poll};
+            SGMM_HIP(hipMemsetAsync(ctl, 0, ws_queue(eps->n), s));
+        }
+#define SGMM_FRONTIER(H_, NSI_)                                                                              \
+    do {                                                                                                     \
+        if (fused)                                                                                           \
+            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, true>), grid, block, 0, s, *ticks, ep, params, src,     \
+                        eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);          \
+        else                                                                                                 \
+            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false>), grid, block, 0, s, *ticks, ep, params, src,    \
+                        eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);          \
+    } while (0)
         if (hidden == 16) {
             if (nsi <= 5) SGMM_FRONTIER(16, 5);
             else SGMM_FRONTIER(16, 8);
@@ -2515,6 +2864,18 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         }
 #undef SGMM_FRONTIER
         SGMM_LAUNCHED();
+        if (fused) {  // the scans (and the GA tail) ran inside; sweep up any left over
+            const int K = step.st ? eps->n / (step.pop_eps > 0 ? step.pop_eps : eps->n) : 0;
+            const dim3 cgrid(std::max(64, std::min(K, 1024)));
+            if (nsi <= 5)
+                SGMM_LAUNCH(k_frontier_cleanup<5>, cgrid, block, 0, s, ep, params, eps->inv_min, cmaps,
+                            reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);
+            else
+                SGMM_LAUNCH(k_frontier_cleanup<8>, cgrid, block, 0, s, ep, params, eps->inv_min, cmaps,
+                            reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);
+            SGMM_LAUNCHED();
+            return SGMM_OK;
+        }
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);

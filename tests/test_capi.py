@@ -68,10 +68,11 @@ def test_argument_errors_need_no_gpu(sgmm):
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
     # frontier kernel (128 chunk slots per episode: u64 map, u32[8] counts, u32 merge info;
-    # u32 wave count per episode) (planes: 1000 ticks + 512 padding slots per episode of the
-    # frontier layout, rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 128 * 8 + 4 * 128 * 32 + 2304
-                                                         + 5 * 3072 * 8)
+    # u32 wave count per episode; then the fused launch's queues: 11 x 128 B of counters + u32
+    # q[8][n], 256-aligned) (planes: 1000 ticks + 528 padding rows per episode of the frontier
+    # layout -- 128-byte aligned episode blocks -- rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 128 * 8 + 4 * 128 * 32 + 2304 + 1536
+                                                         + 5 * 3136 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)
@@ -81,14 +82,14 @@ def test_argument_errors_need_no_gpu(sgmm):
                             ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
     assert rc == -1 and b"bars per day" in L.sgmm_last_error()
     # adversary (20 states): u64 fill words + 64-byte chunk transducers (1000/64 + 4 + 1 slots)
-    # + per-state f64 reward planes (stride 1000 + 512 * 4 rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 3072 * 8
+    # + per-state f64 reward planes (stride 1000 + 528 * 4 rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 3136 * 8
     # ABI 4: the adversary flag is explicit, so 1 or 2 inventory values (4 or 8
     # states) get the adversary layout, not the no-adversary one of the same state count
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 1) == L.sgmm_rollout_workspace_size(4, 1000, 20)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) == L.sgmm_rollout_workspace_size(4, 1000, 5)
     for nsi in (1, 2):
-        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 1280 + 4 * nsi * 3072 * 8
+        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 1280 + 4 * nsi * 3136 * 8
     # the worked example: one 5000-tick ARL episode with 2 inventory values
     assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) > L.sgmm_rollout_workspace_size(1, 5000, 8)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 9, 0) == 0  # more than 8 inventory values

@@ -17,12 +17,15 @@ pytestmark = [pytest.mark.gpu,
 DEV = torch.device("cuda:0")
 
 
-@pytest.fixture(params=[1, 2], ids=["1wave", "2waves"])
+@pytest.fixture(params=[1, 2, "fused"], ids=["1wave", "2waves", "fused"])
 def frontier(monkeypatch, request):
     """The frontier kernel with one wave (64 chunks) or two waves (128 chunks,
-    two independent 64-chunk groups) per episode."""
+    two independent 64-chunk groups) per episode; "fused": one wave per
+    episode with the path scans inside the launch (scanner waves fed by
+    per-XCD queues, then the cleanup launch)."""
     monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_NW", str(request.param))
+    monkeypatch.setenv("SGMM_FRONTIER_NW", "1" if request.param == "fused" else str(request.param))
+    monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if request.param == "fused" else "0")
 
 
 def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
@@ -116,23 +119,46 @@ def test_frontier_lifts_the_episode_length_cap(sgmm, oracle, monkeypatch):
 
 def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
     """DRLEngine (device RNG, fused validation) trains identically with the
-    frontier kernel and with the table: histories and final masters."""
+    frontier kernel, the frontier kernel with its scans and GA tail fused into
+    the launch (the tail then runs in the cleanup launch), and the table:
+    histories and final masters."""
     from sgmm_amd import synthetic
     tr = synthetic.bundle_510300(900, seed=51)
     va = synthetic.bundle_510300(200, seed=52)
     st = synthetic.train_stats(tr)
     out = {}
-    for path in ("table", "frontier"):
-        monkeypatch.setenv("SGMM_TABLE_PATH", path)
+    for path in ("table", "frontier", "fused"):
+        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path == "fused" else path)
+        monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if path == "fused" else "0")
         torch.manual_seed(7)
         eng = sgmm.DRLEngine(pop_size=40, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / path), hidden_dim=32,
                              rng="device", seed=99, sync_every=4, verbose=False)
         pol, hist = eng.train(tr, va, st, generations=10)
         out[path] = (pol.get_weights().numpy(), hist)
-    (wa, ha), (wb, hb) = out["table"], out["frontier"]
-    for k in ha:
-        assert np.array_equal(np.array(ha[k], np.float64), np.array(hb[k], np.float64), equal_nan=True), k
-    assert np.array_equal(wa, wb)
+    wa, ha = out["table"]
+    for path in ("frontier", "fused"):
+        wb, hb = out[path]
+        for k in ha:
+            assert np.array_equal(np.array(ha[k], np.float64), np.array(hb[k], np.float64), equal_nan=True), (path, k)
+        assert np.array_equal(wa, wb), path
+
+
+@pytest.mark.parametrize("val_mode", ["best", "fused"])
+def test_fused_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mode):
+    """Three populations (two assets) trained with the fused frontier launch
+    -- scans by scanner waves, each population's tell (best validation) or
+    whole GA step (fused validation) in the cleanup launch -- equal the table
+    path bit for bit (Env/drl_engine.py:91-171)."""
+    import _shard_ranks as R
+    tr, va, st = R.multi_workload()
+    out = {}
+    for path in ("table", "fused"):
+        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path == "fused" else "table")
+        monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if path == "fused" else "0")
+        m = R.multi_engines(sgmm, 30, False, str(tmp_path / path), val_mode, dist=False)
+        out[path] = R.multi_result(m, m.train(tr, va, st, generations=8))
+    for key in out["table"]:
+        assert np.array_equal(out["table"][key], out["fused"][key], equal_nan=True), key
 
 
 @pytest.mark.parametrize("nw", ["1", "2"], ids=["1wave", "2waves"])

@@ -3,4 +3,4 @@ set -o pipefail
 mkdir -p gpurun_out/fr8
 timeout -k 10 900 python -u -m pytest tests/test_gpu_frontier.py tests/test_gpu_parity.py tests/test_gpu_multi.py tests/test_gpu_ga.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/fr8/pytest.log 2>&1 || { echo PYTEST_FAIL; tail -40 gpurun_out/fr8/pytest.log; exit 1; }
 tail -1 gpurun_out/fr8/pytest.log
-bash tools/ab_lib2.sh fr8 tools/mb/libsgmm_base.so deep-reinforcement-learning-based-signal-gated-market-making_amd/libsgmm.so 2 --config 3 --steps 30
+bash tools/ab_lib2.sh fr8 tools/diag/libsgmm_base.so deep-reinforcement-learning-based-signal-gated-market-making_amd/libsgmm.so 2 --config 3 --steps 30

@@ -8,7 +8,7 @@ import os
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
-os.environ["SGMM_LIB"] = str(ROOT / os.environ.get("STAMP_LIB", "tools/mb/libsgmm_phase.so"))
+os.environ["SGMM_LIB"] = str(ROOT / os.environ.get("STAMP_LIB", "tools/diag/libsgmm_phase.so"))
 os.environ["SGMM_TABLE_PATH"] = "frontier"
 sys.path.insert(0, str(ROOT))
 import numpy as np

@@ -12,7 +12,7 @@ import sys
 import tempfile
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
-os.environ["SGMM_LIB"] = os.environ.get("STAMP_LIB", str(ROOT / "tools/mb/libsgmm_stamps.so"))
+os.environ["SGMM_LIB"] = os.environ.get("STAMP_LIB", str(ROOT / "tools/diag/libsgmm_stamps.so"))
 sys.path.insert(0, str(ROOT))
 import numpy as np
 import torch
