@@ -1282,7 +1282,7 @@ __device__ __forceinline__ void store_record(double* fitness, int32_t* trades, i
 // The GA step of population k once all its records are stored (the last
 // arriver's part of generation_tail; the fused frontier launch's cleanup runs
 // it directly).
-__device__ void tail_run(const StepArgs& sa0, const double* fitness0, const int32_t* trades0, unsigned char* lds,
+__device__ __forceinline__ void tail_run(const StepArgs& sa0, const double* fitness0, const int32_t* trades0, unsigned char* lds,
                          int k, int n_eps) {
     StepArgs sa = sa0;
     sa.st = sa0.st + k;
@@ -1319,7 +1319,7 @@ __device__ void tail_run(const StepArgs& sa0, const double* fitness0, const int3
     SGMM_STAMP(blockIdx.x, 5);
 }
 
-__device__ void generation_tail(const StepArgs& sa0, const double* fitness0, const int32_t* trades0,
+__device__ __forceinline__ void generation_tail(const StepArgs& sa0, const double* fitness0, const int32_t* trades0,
                                 unsigned char* lds, int* s_last, int e, int n_total) {
     // this episode's population (one arrival ticket per population)
     const int n_eps = sa0.pop_eps > 0 ? sa0.pop_eps : n_total;
@@ -1338,7 +1338,7 @@ __device__ void generation_tail(const StepArgs& sa0, const double* fitness0, con
 // The validation launch's tail (StepArgs::mode 2): episode k holds the
 // validation record (v, vtr: thread 0's values) of population k's post-tell
 // master and runs its bookkeeping -- no other episode's record is needed.
-__device__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag, int k) {
+__device__ __forceinline__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag, int k) {
     __syncthreads();  // flag aliases LDS the caller has just read
     val_update_dev(sa.st + k, v, vtr, sa.master_mm + (int64_t)k * sa.n_mm,
                    sa.best_master ? sa.best_master + (int64_t)k * sa.n_mm : nullptr, sa.n_mm,
@@ -1733,8 +1733,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     if (!FUSED && cg == 0 && threadIdx.x == 0) ep.fnw[e] = (uint32_t)nw;  // fused: the queue entry carries it
     const int32_t T = ep.len[e];
 
-    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 4];  // (W3[0][j], W3[1][j]) pairs, then b3
-    __shared__ __attribute__((aligned(16))) float w1x[4][KS];      // W1[4i + g][2] at [g][i]
+    // (13 200 bytes of LDS per wave for H = 32 with `big`: twelve waves fit a
+    // CU's 160 KiB in 512-byte granules, the walks and the scanners of a
+    // 3-waves-per-SIMD grid; 13 328 bytes allowed only eleven)
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
     __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
     __shared__ __attribute__((aligned(16))) float b2s[H];
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
@@ -1759,7 +1761,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
     if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
     if (lane < H) {
-        w1x[lane & 3][lane >> 2] = gsm[L::W1 + 3 * lane + 2];
         l1w[lane][0] = gsm[L::W1 + 3 * lane];
         l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
         l1w[lane][2] = gsm[L::B1 + lane];
@@ -1904,7 +1905,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             constexpr int NQ = decltype(nq)::value;
             lds_cf* w3p = (lds_cf*)(&w3i[0]);
             asm volatile("" : "+v"(w3p));
-            lds_cf* w1p = (lds_cf*)(&w1x[0][0]);
+            lds_cf* w1p = (lds_cf*)(&l1w[0][0]);  // W1[k][2] at l1w[k][3]
             asm volatile("" : "+v"(w1p));
             lds_cf* b2p = (lds_cf*)(&b2s[0]);
             asm volatile("" : "+v"(b2p));
@@ -1919,7 +1920,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             }
 #pragma unroll
             for (int i4 = 0; i4 < KS; i4 += 4) {
-                const f32x4 u = *reinterpret_cast<lds_cf4*>(w1p + grp * KS + i4);
+                float u[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) u[r] = w1p[4 * (4 * (i4 + r) + grp) + 3];
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
 #pragma unroll
