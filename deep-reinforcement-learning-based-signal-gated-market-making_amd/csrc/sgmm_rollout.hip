@@ -5,26 +5,31 @@
 // (Env/market_env.py:22-67), TradingPolicy / AdversaryPolicy
 // (models/model.py:5-57).
 //
-// Fitness path (sgmm_rollout_fitness) -- two kernels:
+// Fitness path (sgmm_rollout_fitness) -- a policy kernel, then a path scan:
 //
-//  1. policy table: the inventory feedback makes an episode a serial chain,
+//  1. policy kernel.  The inventory feedback makes an episode a serial chain,
 //     but the policy only sees (signal_t, inventory) and the inventory takes
-//     at most 8 values (caps +-2 -> 5).  So the policy, the FPT fill test and
-//     the reward are evaluated for EVERY (tick, inventory[, adversary flags])
-//     state in parallel.  H >= 16: k_policy_table_mfma, the H x H layer on
-//     v_mfma_f32_16x16x4_f32 (whose k-ordered fused chain IS the canonical
-//     dot-product order); H = 8 or SGMM_TABLE_PATH=valu: k_policy_table, one
-//     lane per (tick, state) on the VALU.  Output: per 64-tick chunk its
-//     transition byte-map and the trade count along the path from each start
-//     state; per tick the path planes (the reward along the chunk's path from
-//     each start state).  With the adversary: 2 fill bits per (inventory,
-//     previous fills) state (u64) and one float64 reward per state.
+//     at most 8 values (caps +-2 -> 5), so the per-(tick, state) work can be
+//     laid out in parallel:
+//     - k_policy_frontier (many episodes, H = 16 / 32): one wave per episode,
+//       lane = chunk, only the states the chunk's paths occupy are evaluated;
+//     - k_policy_table_v3 (few episodes, and the adversary path): every
+//       (tick, inventory[, adversary flags]) state, one wave per 64 ticks, the
+//       H x H layer on v_mfma_f32_16x16x4_f32 (its k-ordered fused chain IS
+//       the canonical dot-product order); k_policy_table_mfma (round 1's
+//       schedule, H = 64) and k_policy_table (VALU, H = 8) likewise.
+//     Output: per chunk its transition byte-map and the trade count along the
+//     path from each start state, per tick the path planes (the reward along
+//     the chunk's path from each start state).  With the adversary: 2 fill
+//     bits per (inventory, previous fills) state (u64) and one float64 reward
+//     plane per state.
 //
-//  2. path scan (one workgroup per episode): chunk start states from a scan
-//     of the chunk maps, each tick's reward = one row of its chunk's path
+//  2. path scan (one workgroup, or one wave, per episode): chunk start states
+//     from the chunk maps, each tick's reward = one row of its chunk's path
 //     plane, summed in the reference's sequential float64 order (bit-exact,
 //     exact_sum_window), trades from the chunk counts.  The adversary variant
-//     walks the 20-state transducer chunk by chunk.
+//     derives each chunk's transducer from the fill codes, chains them by
+//     pointer jumping segment by segment and walks the true path.
 //
 // Trace path (sgmm_rollout_trace): k_rollout_direct, one wave per episode,
 // lane = hidden neuron, the literal step loop (independent second
@@ -42,7 +47,7 @@ namespace sgmm {
 constexpr int kChunk = 64;          // ticks per chunk in the path scan
 constexpr int kSeg = 4096;          // ticks summed per LDS segment
 constexpr int kScanBlock = 256;
-constexpr int kMaxLen = 1 << 17;    // max ticks per episode (LDS end-map bound)
+constexpr int kMaxLen = 1 << 17;    // max ticks per episode of the no-adversary table path (its scan's LDS chunk tables)
 
 struct EpArrays {
     const int32_t* genome;
@@ -174,40 +179,6 @@ __device__ __forceinline__ int next_state_arl(int s, int code) {
     return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
 }
 
-constexpr int kArlSlot = 64;  // bytes per chunk: end state of each start state [0, 32), trades [32, 64)
-
-// One wave, lane = tick of a 64-tick chunk, fw = the lane's 2-bit fill codes
-// of every state: lanes s < ns walk the chunk from start state s and store
-// its end state and trade count -- the chunk's transducer, so the path scan
-// only chains chunk starts (the scan used to run these ns walks per chunk).
-__device__ void arl_chunk_maps(uint64_t fw, int nvalid, int ns, uint64_t* fwl, uint8_t* __restrict__ slot) {
-    const int lane = threadIdx.x & (kWave - 1);
-    fwl[lane] = lane < nvalid ? fw : 0ull;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    if (lane < ns) {
-        // 8 codes per LDS round trip, then 8 register-only steps of the chain
-        // (padded ticks carry code 0: no fill, the state's flags cleared --
-        // so the walk stops at nvalid)
-        int st = lane, cnt = 0;
-        for (int t8 = 0; t8 < nvalid; t8 += 8) {
-            uint64_t f[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fwl[t8 + j];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                if (t8 + j < nvalid) {
-                    const int c = (int)(f[j] >> (2 * st)) & 3;
-                    cnt += c != 0;
-                    st = next_state_arl(st, c);
-                }
-            }
-        }
-        slot[lane] = (uint8_t)st;
-        slot[32 + lane] = (uint8_t)cnt;
-    }
-}
-
 // ------------------------------------------------------------------ table
 // Block = 64 consecutive ticks of one episode x nsi inventory states: wave w
 // evaluates the policy and the FPT step for every tick of the block from
@@ -223,7 +194,7 @@ __device__ void arl_chunk_maps(uint64_t fw, int nvalid, int ns, uint64_t* fwl, u
 //         rew[s * rs + row] = the reward of the tick along the chunk's path
 //         that starts in state s (float64);
 //    ARL: fills[row] = 2 fill bits per (inventory, sell flag, buy flag) state
-//         and rew[row * ns + state] = the step reward from that state.
+//         and rew[state * rs + row] = the step reward from that state.
 template <int H, int NSM, bool ARL>
 __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params,
@@ -303,13 +274,10 @@ __global__ __launch_bounds__(kChunk * 8) void k_policy_table(
     __syncthreads();
     if (w != 0) return;
     const int64_t row = ep.step_off[e] + t0 + lane;
-    if (ARL) {
+    if (ARL) {  // the fill codes (the scan derives the chunk transducers from them)
         uint64_t fw = 0;
         for (int s = 0; s < ns; ++s) fw |= (uint64_t)code[s][lane] << (2 * s);
         if (valid) fills[row] = fw;
-        __shared__ uint64_t fwl[kWave];
-        arl_chunk_maps(fw, nvalid, ns, fwl,
-                       reinterpret_cast<uint8_t*>(cmaps) + (int64_t)(chunk_base(ep.step_off[e], e) + blockIdx.x) * kArlSlot);
         return;
     }
     uint64_t map = kIdentityMap;
@@ -594,11 +562,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : ((ARL && H <= 32) ? 3 : 1)
             }
         }
     }
-    if (ARL) {
+    if (ARL) {  // the fill codes (the scan derives the chunk transducers from them)
         if (valid) fills[row] = fw;
-        __shared__ uint64_t fwl_s[4][kWave];
-        arl_chunk_maps(fw, min(kChunk, T - t0), ns, fwl_s[threadIdx.x >> 6],
-                       reinterpret_cast<uint8_t*>(cmaps) + (int64_t)(chunk_base(ep.step_off[e], e) + chunk) * kArlSlot);
         return;
     }
     SGMM_TSTAMP(wslot, 3, map + traded);
@@ -643,11 +608,17 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : ((ARL && H <= 32) ? 3 : 1)
 // clamped tick and are masked out of the maps afterwards), so a region is a
 // single basic block.  Packed f32 FMAs are avoided beside the MFMAs (a
 // v_pk_fma_f32 there costs ~22 cycles more than two v_fma_f32).
-template <int H, int NSI, int MODE>
+// ARL (MODE 1 only): the adversary's state space (inventory x previous fill
+// flags, 4 nsi states): state si's policy outputs drive the FPT step from its
+// four flag states (adversary deltas from a per-episode LUT), each reward
+// goes straight to its per-state plane and the tick's 2-bit fill codes to
+// fills[row] -- k_policy_table_mfma's outputs.
+template <int H, int NSI, int MODE, bool ARL>
 __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k_policy_table_v3(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
     int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
-    double* __restrict__ rew) {
+    uint64_t* __restrict__ fills, double* __restrict__ rew) {
+    static_assert(!ARL || MODE == 1, "adversary: the one-accumulator schedule");
     static_assert(H % 16 == 0 && H <= 32, "v3 table: H = 16 or 32");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16;   // 16-neuron row tiles of layer 2
@@ -680,8 +651,20 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
     __shared__ __attribute__((aligned(16))) double rl_s[4][NSI][kWave];  // [state][lane] path-plane rewards
     static_assert(sizeof(rl_s) >= sizeof(float) * L::N, "genome fits the reward buffer");
     float* gsm = reinterpret_cast<float*>(&rl_s[0][0][0]);
-    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __shared__ float gsa[ARL ? kAdvParams : 1];
+    __shared__ int32_t lut[2][ARL ? 32 : 1];  // adversary deltas (bid, ask) per state
+    const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
+    stage_genomes(src, e, ep.genome[e], ai, L::N, gsm, ARL ? gsa : nullptr);
     __syncthreads();
+    if constexpr (ARL) {
+        if ((int)threadIdx.x < 4 * nsi) {
+            const int st = threadIdx.x;
+            int32_t da = 0, db = 0;
+            if (ai >= 0) adv_delta(gsa, params[ep.param[e]], inv_min + (st >> 2), (st >> 1) & 1, st & 1, da, db);
+            lut[0][st] = da;
+            lut[1][st] = db;
+        }
+    }
     __shared__ __attribute__((aligned(16))) float w3i[2 * H];  // (W3[0][j], W3[1][j]) pairs
     if (threadIdx.x < 2 * H) w3i[threadIdx.x] = gsm[L::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
     const float* g = gsm;
@@ -724,6 +707,9 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
     f32x4 acc[MODE == 0 ? 2 : 1][4][NT];
     uint64_t map = kIdentityMap;
     uint32_t traded = 0;
+    uint64_t fw = 0;  // ARL: 2 fill bits per state
+    const bool valid = t0 + lane < T;
+    const int64_t row = ep.step_off[e] + t0 + lane;
     auto layer12 = [&](int si, int b) {  // layer 1 (VALU) + layer 2 (MFMA) of state si into set b
         const float x2 = (float)((double)(inv_min + si) / 2.0);
 #pragma unroll
@@ -764,12 +750,25 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
         }
         const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
         const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-        const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
-        const bool live = si < nsi;  // states past the caps keep the identity byte
-        const uint64_t to = live ? (uint64_t)(si + so.fill_buy - so.fill_sell) : (uint64_t)si;
-        map = (map & ~(0xFFull << (8 * si))) | (to << (8 * si));
-        traded |= (uint32_t)(live && (so.fill_buy | so.fill_sell)) << si;
-        rl[si * kWave + lane] = so.reward;
+        if constexpr (ARL) {
+            if (si < nsi) {  // uniform
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int st = 4 * si + c;
+                    const StepOut so = ftp_step(p, inv_min + si, oa + lut[0][st], ob + lut[1][st], tmid, task, tbid,
+                                                tbmax, tsmin);
+                    fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * st);
+                    if (valid) rew[st * ep.rs + row] = so.reward;  // per-state planes (SoA): coalesced rows
+                }
+            }
+        } else {
+            const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
+            const bool live = si < nsi;  // states past the caps keep the identity byte
+            const uint64_t to = live ? (uint64_t)(si + so.fill_buy - so.fill_sell) : (uint64_t)si;
+            map = (map & ~(0xFFull << (8 * si))) | (to << (8 * si));
+            traded |= (uint32_t)(live && (so.fill_buy | so.fill_sell)) << si;
+            rl[si * kWave + lane] = so.reward;
+        }
     };
     if constexpr (MODE == 0) {
         layer12(0, 0);
@@ -830,8 +829,11 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    SGMM_TSTAMP(wslot, 2, map + traded);
-    const bool valid = t0 + lane < T;
+    SGMM_TSTAMP(wslot, 2, map + traded + fw);
+    if constexpr (ARL) {
+        if (valid) fills[row] = fw;
+        return;
+    }
     if (!valid) {  // padded lanes: identity steps, no trades
         map = kIdentityMap;
         traded = 0;
@@ -842,7 +844,6 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
     SGMM_TSTAMP(wslot, 3, excl);
     // path planes: plane s holds the reward along the chunk's path from start
     // state s; per start state the path's trade count (8 bits each)
-    const int64_t row = ep.step_off[e] + t0 + lane;
     uint64_t cnt = 0;
 #pragma unroll
     for (int s0 = 0; s0 < NSI; ++s0) {
@@ -2263,80 +2264,118 @@ __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __re
 
 
 // ------------------------------------------------------------------ path scan (adversary)
-// 20-state transducer (inventory x previous fills): every chunk is walked from
-// every start state, the chunk end-maps are chained, each chunk is replayed
-// from its true start.  Dynamic LDS: [kSeg doubles][nch*ns end maps][nch starts]
-__global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
+// 4 nsi-state machine (inventory x previous fill flags).  Per episode, one
+// NT-thread workgroup, segment by segment (kSeg ticks = 64 chunks of 64), the
+// state entering a segment carried over -- no bound on the episode length:
+//   1. the segment's fill codes -> LDS (coalesced);
+//   2. every (chunk, start state) pair walks its chunk over the LDS codes (8
+//      per round trip): the chunk's transducer, end state and trade count per
+//      start state (all NT threads: ~1 round of 64 steps at config 4, where
+//      one serial walker per table wave cost the table ~25 us);
+//   3. the end maps chained by pointer jumping (log2(64) rounds over all
+//      (chunk, state) pairs) -> each chunk's start state; trades = the sum of
+//      every chunk's count from its start state;
+//   4. one thread per chunk walks its 64 ticks from the start state and
+//      records the state of every tick;
+//   5. every thread gathers its ticks' rewards from the per-state planes
+//      rew[state * rs + row] (independent loads: one latency per segment;
+//      consecutive ticks in one state are consecutive addresses);
+//   6. the exact sequential float64 sum (exact_sum_window).
+// Dynamic LDS: [kSeg u64 codes / f64 rewards][kSeg states][2][64][ns] maps
+// [64][ns] trade counts [64] starts.
+constexpr int kSegChunks = kSeg / kChunk;
+static size_t arl_scan_lds(int ns) { return (size_t)kSeg * 9 + (size_t)3 * kSegChunks * ns + kSegChunks; }
+template <int NT>
+__global__ __launch_bounds__(NT) void k_path_scan_arl(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, int32_t nsi,
-    const uint64_t* __restrict__ fills, const uint8_t* __restrict__ chunks, const double* __restrict__ rew,
+    const uint64_t* __restrict__ fills, const double* __restrict__ rew,
     double* __restrict__ fitness, int32_t* __restrict__ trades_out, StepArgs step) {
-    // chunks: per 64-tick chunk the table's transducer (end state and trade
-    // count from each of the ns start states, kArlSlot bytes); rew: per-state
-    // reward planes rew[s * rs + row].  Per episode:
-    //   1. the chunks' start states: the end maps chained by pointer jumping
-    //      (log2(chunks) rounds over all (chunk, state) pairs, no serial lane),
-    //      trades = the sum of every chunk's count from its start state;
-    //   2. per 4096-tick segment, one thread per chunk walks its 64 ticks
-    //      from the start state with the fill codes and gathers the rewards
-    //      from the per-state planes (consecutive ticks of one state are
-    //      consecutive addresses);
-    //   3. the exact sequential float64 sum.
     extern __shared__ __align__(16) unsigned char lds[];
-    double* sel = reinterpret_cast<double*>(lds);
-    __shared__ SumLds<kScanBlock> L;
+    uint64_t* fl = reinterpret_cast<uint64_t*>(lds);  // the segment's fill codes, then
+    double* sel = reinterpret_cast<double*>(lds);     // its rewards (the codes are dead by then)
+    uint8_t* stt = lds + kSeg * sizeof(double);       // [kSeg] the state at each tick
+    const int ns = 4 * nsi;
+    uint8_t* jm = stt + kSeg;                         // [2][segch][ns] jump maps (double-buffered)
+    uint8_t* tr = jm + 2 * kSegChunks * ns;           // [segch][ns] trades from each start state
+    uint8_t* start = tr + kSegChunks * ns;            // [segch]
+    __shared__ SumLds<NT> L;
+    __shared__ int red_trades;
     const int e = blockIdx.x;
     const int32_t T = ep.len[e];
-    const int ns = 4 * nsi;
-    const int nch = (T + kChunk - 1) / kChunk;
-    uint8_t* jm = lds + kSeg * sizeof(double);   // [2][nch][ns] jump maps (double-buffered)
-    uint8_t* start = jm + 2 * nch * ns;          // [nch]
-    __shared__ int red_trades;
     const int64_t so = ep.step_off[e];
     const uint64_t* __restrict__ F = fills + so;
-    const uint8_t* __restrict__ C = chunks + (int64_t)chunk_base(so, e) * kArlSlot;
     const int tid = threadIdx.x;
     if (tid == 0) red_trades = 0;
-    // jm[k][s] = state after chunks k-2^r+1 .. k from state s at chunk k-2^r+1's start
-    for (int i = tid; i < nch * ns; i += kScanBlock) jm[i] = C[(i / ns) * kArlSlot + i % ns];
-    __syncthreads();
-    int cur = 0;
-    for (int d = 1; d < nch; d <<= 1) {
-        const uint8_t* a = jm + cur * nch * ns;
-        uint8_t* b = jm + (cur ^ 1) * nch * ns;
-        for (int i = tid; i < nch * ns; i += kScanBlock) {
-            const int k = i / ns, st = i - k * ns;
-            b[i] = k >= d ? a[k * ns + a[(k - d) * ns + st]] : a[i];
-        }
-        cur ^= 1;
-        __syncthreads();
-    }
-    // start of chunk k = inclusive prefix of chunks 0 .. k-1 applied to the episode start
-    const int s0 = (-inv_min) << 2;
-    const uint8_t* pre = jm + cur * nch * ns;
+    int carry = (-inv_min) << 2;  // the state entering the segment (episode start: inventory 0, no fills)
     int my_trades = 0;
-    for (int k = tid; k < nch; k += kScanBlock) {
-        const int st = k == 0 ? s0 : pre[(k - 1) * ns + s0];
-        start[k] = (uint8_t)st;
-        my_trades += C[k * kArlSlot + 32 + st];
-    }
-    __syncthreads();
     double total = 0.0;
     for (int seg0 = 0; seg0 < T; seg0 += kSeg) {
         const int segn = min(kSeg, T - seg0);
         const int segch = (segn + kChunk - 1) / kChunk;
-        if (tid < segch) {
-            const int k = seg0 / kChunk + tid;
-            int s = start[k];
-            const int ta = k * kChunk, tb = min(T, ta + kChunk);
-            for (int t = ta; t < tb; ++t) {
-                const int code = (int)(F[t] >> (2 * s)) & 3;
-                sel[t - seg0] = rew[(int64_t)s * ep.rs + so + t];
-                s = next_state_arl(s, code);
+        for (int i = tid; i < segn; i += NT) fl[i] = F[seg0 + i];
+        __syncthreads();
+        // chunk k's transducer from start state s (padded ticks: none, the walk stops at the chunk's end)
+        for (int i = tid; i < segch * ns; i += NT) {
+            const int k = i / ns;
+            int st = i - k * ns, cnt = 0;
+            const int ta = k * kChunk, tb = min(segn, ta + kChunk);
+            for (int t8 = ta; t8 < tb; t8 += 8) {
+                uint64_t f[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] = fl[t8 + j];  // < kSeg: in the buffer
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (t8 + j < tb) {
+                        const int c = (int)(f[j] >> (2 * st)) & 3;
+                        cnt += c != 0;
+                        st = next_state_arl(st, c);
+                    }
             }
+            jm[i] = (uint8_t)st;
+            tr[i] = (uint8_t)cnt;
         }
         __syncthreads();
-        for (int k = 0; k < segn; k += 4 * kScanBlock)  // windows of 4 values per thread
-            total = exact_sum_window<kScanBlock>(sel + k, min(4 * kScanBlock, segn - k), total, L);
+        // jm[k][s] = state after chunks k-2^r+1 .. k from state s at chunk k-2^r+1's start
+        int cur = 0;
+        for (int d = 1; d < segch; d <<= 1) {
+            const uint8_t* a = jm + cur * segch * ns;
+            uint8_t* b = jm + (cur ^ 1) * segch * ns;
+            for (int i = tid; i < segch * ns; i += NT) {
+                const int k = i / ns, st = i - k * ns;
+                b[i] = k >= d ? a[k * ns + a[(k - d) * ns + st]] : a[i];
+            }
+            cur ^= 1;
+            __syncthreads();
+        }
+        // start of chunk k = the inclusive prefix of chunks 0 .. k-1 applied to the carry
+        const uint8_t* pre = jm + cur * segch * ns;
+        for (int k = tid; k < segch; k += NT) {
+            const int st = k == 0 ? carry : pre[(k - 1) * ns + carry];
+            start[k] = (uint8_t)st;
+            my_trades += tr[k * ns + st];
+        }
+        __syncthreads();
+        carry = pre[(segch - 1) * ns + carry];
+        if (tid < segch) {  // chunk tid's state path
+            int st = start[tid];
+            const int ta = tid * kChunk, tb = min(segn, ta + kChunk);
+            for (int t8 = ta; t8 < tb; t8 += 8) {
+                uint64_t f[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) f[j] = fl[t8 + j];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (t8 + j < tb) {
+                        stt[t8 + j] = (uint8_t)st;
+                        st = next_state_arl(st, (int)(f[j] >> (2 * st)) & 3);
+                    }
+            }
+        }
+        __syncthreads();  // the codes are dead: sel takes their place
+        for (int i = tid; i < segn; i += NT) sel[i] = rew[(int64_t)stt[i] * ep.rs + so + seg0 + i];
+        __syncthreads();
+        for (int k = 0; k < segn; k += 4 * NT)  // windows of 4 values per thread
+            total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L);
     }
     int w = my_trades;
 #pragma unroll
@@ -2344,9 +2383,9 @@ __global__ __launch_bounds__(kScanBlock) void k_path_scan_arl(
     if ((tid & (kWave - 1)) == 0 && w) atomicAdd(&red_trades, w);
     __syncthreads();
     if (tid == 0) {
-        const int tr = red_trades;
-        if (tr == 0) total -= params[ep.param[e]].idle_penalty;
-        store_record(fitness, trades_out, e, total, tr);
+        const int tr_ = red_trades;
+        if (tr_ == 0) total -= params[ep.param[e]].idle_penalty;
+        store_record(fitness, trades_out, e, total, tr_);
     }
     if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades, e, (int)gridDim.x);
 }
@@ -2559,6 +2598,7 @@ static int table_path() {
     if (e && std::strcmp(e, "valu") == 0) return 1;
     if (e && std::strcmp(e, "v2") == 0) return 2;  // k_policy_table_mfma without the v3 schedule
     if (e && std::strcmp(e, "v3i") == 0) return 3;  // v3 with two accumulator sets, blocks interleaved
+    if (e && std::strcmp(e, "v3") == 0) return 4;   // v3 (the default without the adversary; opt-in with it)
     return 0;
 }
 
@@ -2611,9 +2651,8 @@ static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(u
 // or two inventory values, so a state count alone cannot tell the layouts apart.
 static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t nsi, bool arl) {
     if (total_steps < 0 || nsi <= 0 || nsi > 8 || n_episodes < 0) return 0;
-    if (arl)  // fill codes, chunk transducers, per-state planes rew[state * rs + row]
-        return ws_fills(total_steps) + align256(n_chunk_slots(n_episodes, total_steps) * kArlSlot) +
-               (size_t)rew_stride(total_steps, n_episodes) * (size_t)(4 * nsi) * sizeof(double);
+    if (arl)  // fill codes, per-state planes rew[state * rs + row]
+        return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes) * (size_t)(4 * nsi) * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
            (size_t)rew_stride(total_steps, n_episodes) * (size_t)nsi * sizeof(double);
 }
@@ -2695,10 +2734,22 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
     if constexpr (H <= 32) {
         const int tp = table_path();
-        if (!arl && (tp == 0 || tp == 3)) {
+        // the adversary on the v3 schedule: opt-in (SGMM_TABLE_PATH=v3) -- measured
+        // slower than k_policy_table_mfma's there (config 4: 159.5 vs 153-155 us; the
+        // 4 FPT steps per state weigh on the vector block the MFMA stream waits for)
+        if (arl && tp == 4) {
+            if (nsi <= 5)
+                SGMM_LAUNCH((k_policy_table_v3<H, 5, 1, true>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi,
+                            ctr, cmaps, fills, rew);
+            else
+                SGMM_LAUNCH((k_policy_table_v3<H, 8, 1, true>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi,
+                            ctr, cmaps, fills, rew);
+            return;
+        }
+        if (!arl && (tp == 0 || tp == 3 || tp == 4)) {
 #define SGMM_TABLE_V3(NSI_, MODE_)                                                                       \
-    SGMM_LAUNCH((k_policy_table_v3<H, NSI_, MODE_>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, \
-                ctr, cmaps, rew)
+    SGMM_LAUNCH((k_policy_table_v3<H, NSI_, MODE_, false>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, \
+                ctr, cmaps, fills, rew)
             if (tp == 3) {
                 if (nsi <= 5) SGMM_TABLE_V3(5, 0);
                 else SGMM_TABLE_V3(8, 0);
@@ -2804,9 +2855,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
-        cmaps = reinterpret_cast<uint64_t*>(w + ws_fills(eps->total_steps));  // chunk transducers
-        rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps) +
-                                        align256(n_chunk_slots(eps->n, eps->total_steps) * kArlSlot));
+        rew = reinterpret_cast<double*>(w + ws_fills(eps->total_steps));
     } else {
         const size_t a = ws_cmaps(eps->n, eps->total_steps), b = ws_ctr(eps->n, eps->total_steps);
         cmaps = reinterpret_cast<uint64_t*>(w);
@@ -2821,8 +2870,9 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ep.fnw = kinfo + n_frontier_slots(eps->n);
     }
     const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
-    SGMM_REQUIRE(fr || eps->max_len <= kMaxLen,
-                 "max_len=%d > %d needs the frontier kernel (no adversary, hidden 16 or 32)", eps->max_len, kMaxLen);
+    SGMM_REQUIRE(fr || arl || eps->max_len <= kMaxLen,
+                 "max_len=%d > %d needs the frontier kernel (hidden 16 or 32) or the adversary path", eps->max_len,
+                 kMaxLen);
     SGMM_REQUIRE(!fr || eps->max_len <= kFrontierMaxLen, "max_len=%d > %lld ticks per episode",
                  eps->max_len, (long long)kFrontierMaxLen);
     // the fused launch: walks and scans in one kernel (the GA tail included);
@@ -2900,13 +2950,19 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         }
         SGMM_LAUNCHED();
     }
-    const int nch_max = (eps->max_len + kChunk - 1) / kChunk;
     ProfScope prof(vt ? "val_path_scan" : "path_scan", s);
     if (arl) {
-        size_t lds = kSeg * sizeof(double) + (size_t)2 * nch_max * ns + nch_max;
-        if (step.st) lds = std::max(lds, step_lds_bytes(kScanBlock, step));
-        SGMM_LAUNCH(k_path_scan_arl, dim3(eps->n), dim3(kScanBlock), lds, s, ep, params, eps->inv_min, nsi,
-                    fills, reinterpret_cast<const uint8_t*>(cmaps), rew, fitness, trades, step);
+        // 16-wave workgroups while one per CU fits (a 4096-tick segment is one
+        // exact-sum window), 4-wave ones beyond
+        const int nt = eps->n <= kScanAt512 ? kScanThreads : kScanBlock;
+        size_t lds = arl_scan_lds(ns);
+        if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
+        if (nt == kScanThreads)
+            SGMM_LAUNCH(k_path_scan_arl<kScanThreads>, dim3(eps->n), dim3(nt), lds, s, ep, params, eps->inv_min,
+                        nsi, fills, rew, fitness, trades, step);
+        else
+            SGMM_LAUNCH(k_path_scan_arl<kScanBlock>, dim3(eps->n), dim3(nt), lds, s, ep, params, eps->inv_min,
+                        nsi, fills, rew, fitness, trades, step);
     } else {
         // the workgroup shrinks as episodes grow: few episodes get a 16-wave
         // workgroup each (4096-tick windows, the phases spread over the CU);

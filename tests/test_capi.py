@@ -81,15 +81,15 @@ def test_argument_errors_need_no_gpu(sgmm):
     rc = L.sgmm_bar_windows(ctypes.byref(ev), 1, ctypes.c_void_p(8), ctypes.c_void_p(8), ctypes.c_void_p(8),
                             ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
     assert rc == -1 and b"bars per day" in L.sgmm_last_error()
-    # adversary (20 states): u64 fill words + 64-byte chunk transducers (1000/64 + 4 + 1 slots)
-    # + per-state f64 reward planes (stride 1000 + 528 * 4 rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 1280 + 20 * 3136 * 8
+    # adversary (20 states): u64 fill words + per-state f64 reward planes (stride
+    # 1000 + 528 * 4 rounded to 32); the scan derives the chunk transducers itself
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 20 * 3136 * 8
     # ABI 4: the adversary flag is explicit, so 1 or 2 inventory values (4 or 8
     # states) get the adversary layout, not the no-adversary one of the same state count
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 1) == L.sgmm_rollout_workspace_size(4, 1000, 20)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) == L.sgmm_rollout_workspace_size(4, 1000, 5)
     for nsi in (1, 2):
-        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 1280 + 4 * nsi * 3136 * 8
+        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 4 * nsi * 3136 * 8
     # the worked example: one 5000-tick ARL episode with 2 inventory values
     assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) > L.sgmm_rollout_workspace_size(1, 5000, 8)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 9, 0) == 0  # more than 8 inventory values

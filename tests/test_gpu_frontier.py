@@ -29,7 +29,7 @@ def frontier(monkeypatch, request):
 
 
 def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
-         n_threads=8):
+         n_threads=8, arl=False):
     from sgmm_amd import synthetic
     lens = np.asarray(lens, np.int64)
     P = len(lens)
@@ -37,6 +37,7 @@ def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=
     b = synthetic.bundle_510300(max(T, 1), seed=seed, nan_frac=nan_frac)
     st = synthetic.train_stats(b)
     pop = synthetic.population(P, H, sigma=sigma, seed=seed + 1)
+    adv = synthetic.population(P, 32, sigma=0.05, seed=seed + 2) if arl else None
     i_max, i_min = caps
     ticks = sgmm.TickStore()
     seg = ticks.add(b, st)
@@ -45,9 +46,12 @@ def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=
     params = sgmm.params_tensor([cfg], DEV)
     eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
                            inv_min=i_min, inv_max=i_max).to(DEV)
-    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
+    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H,
+                                               adv.to(DEV) if arl else None)
     s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
-    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, adv.numpy() if arl else None,
+                                           (s1n, s2n) + tuple(b[2:]), np.arange(P),
+                                           np.arange(P) if arl else None,
                                            np.zeros(P), lens, np.zeros(P),
                                            [oracle.params(phi=phi, tick=0.001, fee=fee, i_max=i_max, i_min=i_min)],
                                            n_threads=n_threads)
@@ -96,25 +100,26 @@ def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw)
     assert np.array_equal(fit, wf)
 
 
-def test_frontier_lifts_the_episode_length_cap(sgmm, oracle, monkeypatch):
+def test_frontier_lifts_the_episode_length_cap(sgmm, oracle):
     """Episodes longer than the table's 131072-tick cap run on the frontier
     kernel (agent_trainer.py:74-77 concatenates days without a bound): a
-    300 000-tick episode bit-exact; forcing the table path fails cleanly."""
+    300 000-tick episode bit-exact."""
     fit, trd, wf, wt = _run(sgmm, oracle, [300000, 131073, 5], 32, seed=49, sigma=0.1)
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
-    from sgmm_amd import synthetic
-    b = synthetic.bundle_510300(131073, seed=1)
-    st = synthetic.train_stats(b)
-    ticks = sgmm.TickStore()
-    seg = ticks.add(b, st)
-    ticks.to(DEV)
-    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.001, tick_size=0.001)], DEV)
-    eb = sgmm.EpisodeBatch([0], [ticks.segments[seg][0]], [131073], [0]).to(DEV)
-    adv = synthetic.population(1, 32, seed=2).to(DEV)
-    from sgmm_amd._lib import SgmmError
-    with pytest.raises(SgmmError, match="frontier"):  # the adversary path has no frontier kernel
-        sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, synthetic.population(1, 32, seed=3).to(DEV), 32, adv)
+
+
+@pytest.mark.parametrize("H", [16, 32])
+def test_adversary_episodes_have_no_length_cap(sgmm, oracle, H):
+    """The adversary path (drl_engine.py:43-48,97-100) has no episode cap
+    either: its scan chains the chunk transducers segment by segment (4096
+    ticks, the state entering each segment carried over), so a 300 000-tick
+    ARL episode -- 74 segments -- and 131 073 / 4097 / 4096 / 5 / 0-tick ones
+    are bit-exact against the oracle."""
+    fit, trd, wf, wt = _run(sgmm, oracle, [300000, 131073, 4097, 4096, 5, 0], H, seed=53, sigma=0.1, arl=True)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+    assert trd[0] > 1000
 
 
 def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
@@ -162,12 +167,11 @@ def test_fused_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, v
 
 
 @pytest.mark.parametrize("nw", ["1", "2"], ids=["1wave", "2waves"])
-def test_frontier_one_wave_scan_row_gather(sgmm, oracle, monkeypatch, nw):
-    """Above 1024 episodes the path scan is one wave per episode and gathers
-    windows of W = 1024 // CL whole chunks row by row (consecutive lanes =
-    consecutive chunks of a plane row): W from 2 to past 64, the per-lane
-    4-tick gather once CL > 512 (W < 2), ragged last windows and chunks,
-    both chunk groups of split episodes -- bit-exact against the oracle."""
+def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
+    """Above 1024 episodes the path scan is one wave per episode (1024-tick
+    windows of a 256-thread layout run by 64 lanes): chunk lengths from 4 to
+    past 512 ticks, ragged last windows and chunks, both chunk groups of split
+    episodes -- bit-exact against the oracle."""
     monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
     monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
     base = np.array([17, 255, 4560, 8191, 20001, 30003, 40000, 4097])
