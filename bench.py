@@ -323,7 +323,7 @@ def main():
     gen_kernel_us = sum(v["avg_us"] * v["launches"] for v in kernels.values()) / max(1, n_prof)
 
     # roofline of the policy kernel (the FP32 compute kernel of the path): the
-    # frontier kernel from 2048 episodes per launch, the table below that
+    # frontier kernel from 768 episodes per launch (the measured crossover), the table below that
     best_val = bool(sess.best_val)
     # the training launch: training episodes (+ every validation episode when fused)
     steps_per_launch = K * n_rank * (T if best_val else T + Tv)

@@ -35,6 +35,7 @@
 // lane = hidden neuron, the literal step loop (independent second
 // implementation; the tests require both paths to agree bit for bit).
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 
@@ -63,6 +64,12 @@ struct EpArrays {
     // policy kernel records each episode's wave count in fnw[e] for the scan
     int32_t fwhole;
     uint32_t* fnw;
+    // frontier kernel, whole episodes: the chunks' tick ranges may be cut into
+    // up to kFrontierSegs segments walked by different waves (a walk hands the
+    // second half of its remaining ticks to an idle wave): fseg[4 e] = segments
+    // allocated (1 + hand-offs; >= kFrontierSegs when one was refused), fseg[4 e
+    // + k] = the chunk tick offset where segment k starts (segment 0 at 0)
+    uint32_t* fseg;
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -898,7 +905,10 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 }
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
 constexpr int kFrontierMaxWaves = 2;   // waves (64-chunk groups) per episode
-constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunk slots per episode
+constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunks per episode (plane padding)
+constexpr int kFrontierSegs = 4;       // tick segments per chunk of a whole episode (hand-offs + 1)
+constexpr int kFrontierRecs = kFrontierLanes * kFrontierSegs;  // chunk records per episode: e * 256 + k * 64 + c
+static_assert(kFrontierRecs >= kFrontierSlots, "records cover both layouts");
 constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
 typedef __attribute__((address_space(3))) const float lds_cf;
 typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
@@ -1387,10 +1397,53 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     const int CL = FR ? frontier_len(T, nw) : kChunk;
     const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
-    const int64_t cb = FR ? (int64_t)e * kFrontierSlots : (int64_t)chunk_base(so, e);
+    const int64_t cb = FR ? (int64_t)e * kFrontierRecs : (int64_t)chunk_base(so, e);
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
+    // segmented chunks (whole frontier episodes whose walks handed ticks over):
+    // the segments in tick order -- ord[j] = record block of the j-th, bnd[j] =
+    // its first chunk offset (INT_MAX past the last); uniform
+    int nseg = 1, ord[kFrontierSegs] = {0, 1, 2, 3}, bnd[kFrontierSegs] = {0, INT_MAX, INT_MAX, INT_MAX};
+    if (FR && nw == 1 && ep.fseg) {
+        nseg = (int)min((uint32_t)kFrontierSegs, ld_rec<SC1>(ep.fseg + 4 * (int64_t)e));
+        for (int k = 1; k < nseg; ++k) bnd[k] = (int)ld_rec<SC1>(ep.fseg + 4 * (int64_t)e + k);
+        for (int k = 1; k < nseg; ++k)  // insertion sort by offset (segment 0 starts at 0)
+            for (int j = k; j > 1 && bnd[j] < bnd[j - 1]; --j) {
+                const int tb_ = bnd[j], to_ = ord[j];
+                bnd[j] = bnd[j - 1];
+                ord[j] = ord[j - 1];
+                bnd[j - 1] = tb_;
+                ord[j - 1] = to_;
+            }
+    }
     SGMM_STAMP(e, 0);
-    if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
+    if (FR && nseg > 1) {  // one round (a whole episode has <= 64 chunks), per chunk its segments in order
+        if (tid < kWave) {
+            const int c = lane;
+            uint64_t mk[kFrontierSegs], M = kIdentityMap;
+#pragma unroll
+            for (int j = 0; j < kFrontierSegs; ++j) {
+                mk[j] = (j < nseg && c < nch) ? ld_rec<SC1>(cmaps + cb + ord[j] * kFrontierLanes + c) : kIdentityMap;
+                M = map_then(M, mk[j]);
+            }
+            const uint64_t inc = wave_map_scan(M);
+            uint64_t excl = shfl_up_u64(inc, 1);
+            if (lane == 0) excl = kIdentityMap;
+            uint32_t st = map_get(excl, (uint32_t)(-inv_min));
+            int tr = 0;
+#pragma unroll
+            for (int j = 0; j < kFrontierSegs; ++j)
+                if (j < nseg && c < nch) {
+                    const int v = ord[j] * kFrontierLanes + c;
+                    start[v] = (uint8_t)st;
+                    tr += (int)ld_rec<SC1>(reinterpret_cast<const uint32_t*>(ctr) + (cb + v) * 8 + st);
+                    kin[v] = ld_rec<SC1>(kinfo + cb + v);
+                    st = map_get(mk[j], st);
+                }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, kWave);
+            if (lane == 0) *sh.red = tr;
+        }
+    } else if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
         uint32_t s = (uint32_t)(-inv_min);
         int tr = 0;
         for (int c0 = 0; c0 < nch; c0 += kWave) {
@@ -1439,9 +1492,12 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
             if (i0 < n) {
                 if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
                     const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
-                    const uint32_t ki = kin[c];
+                    // the record of the segment holding offset u (segment offsets are
+                    // multiples of kSumTpt: a thread's ticks lie in one segment)
+                    const int v = ord[(u >= bnd[1]) + (u >= bnd[2]) + (u >= bnd[3])] * kFrontierLanes + c;
+                    const uint32_t ki = kin[v];
                     const int kc = (int)(ki & 0x1FFFFFFFu);
-                    const int64_t pst = start[c], pp0 = ki >> 29;
+                    const int64_t pst = start[v], pp0 = ki >> 29;
                     const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        c % kFrontierLanes;
 #pragma unroll
@@ -1516,8 +1572,8 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[FR ? kFrontierSlots : kMaxLen / kChunk];
-    __shared__ uint32_t kin[FR ? kFrontierSlots : 1];
+    __shared__ uint8_t start[FR ? kFrontierRecs : kMaxLen / kChunk];
+    __shared__ uint32_t kin[FR ? kFrontierRecs : 1];
     __shared__ int red_trades;
     const int e = blockIdx.x;
     const ScanShared<NT> sh{reinterpret_cast<double*>(lds), &L, start, kin, &red_trades, lds};
@@ -1563,8 +1619,8 @@ __device__ __forceinline__ uint32_t xcc_id() {
 }
 constexpr int kFusedScanNT = 4 * kWave;                             // one-wave scans: 256-thread window layout
 constexpr int kFusedSel = kFusedScanNT * kSumTpt * (int)sizeof(double);  // 8 KB window
-constexpr int kFusedScanLds = kFusedSel + (int)sizeof(SumLds<kFusedScanNT>) + kFrontierSlots +
-                              4 * kFrontierSlots + 16;
+constexpr int kFusedScanLds = kFusedSel + (int)sizeof(SumLds<kFusedScanNT>) + kFrontierRecs +
+                              4 * kFrontierRecs + 16;
 static_assert(sizeof(SumLds<kFusedScanNT>) % 8 == 0, "scan LDS carve-out alignment");
 
 template <class T>
@@ -1589,6 +1645,43 @@ __device__ __forceinline__ uint64_t* queue_state(const FrontierQueue& fq, uint32
 
 typedef __attribute__((address_space(3))) unsigned char lds_u8;
 
+// Tick hand-offs between frontier walks (not in the fused launch).  A wave
+// whose walk has ended waits as a helper (while every walk of the launch has
+// started); a walk that sees a helper waiting, with >= min_rem ticks left in
+// its segment, hands the second half of them to the queue: a new segment of
+// the episode's chunks, walked from its first tick with every start state
+// tracked (its start state is known only to the scan), written to its own
+// records.  The walk's paths from a segment start are the same paths, so the
+// outputs stay bit-identical; the tail of the launch (the heaviest walks alone
+// on their SIMDs) is shared out instead.  ctl words, one 128-byte line each:
+// [0] queue head, [32] queue tail, [64] items (walks + segments) not yet
+// finished, [96] helpers waiting, [128] walks started; then the episodes'
+// segment tables (EpArrays::fseg, u32[4 n]), then the queue: q[i] = item i
+// (0 = not yet stored): (e + 1) | segment << 28 | start << 32 | end << 48.
+constexpr int kStHead = 0, kStTail = 32, kStActive = 64, kStIdle = 96, kStStarted = 128;
+constexpr int kStNoSlot = 129, kStQuitEarly = 130;  // diagnostics: refused hand-offs, helpers that left early
+constexpr int kStHelpers = 131;  // waves that became helpers (at most FrontierSteal::max_helpers)
+constexpr int kStCtlWords = 160;
+constexpr int kStealMinRem = 16;  // ticks left in a segment for a hand-off (two halves of >= 8)
+struct FrontierSteal {
+    uint32_t* ctl;  // ctl[kStCtlWords] | fseg[4 n] | u64 q[3 n + 64]
+    int32_t on;
+    int32_t nwalk;
+    int32_t n;      // episodes of the launch
+    int32_t maxseg; // segments per episode allowed (<= kFrontierSegs)
+    int32_t helper_every;  // the finished waves of blocks b % helper_every == 0 stay as helpers
+    int32_t nchk;          // hand-off checks per segment (from half-way, every eighth)
+    __device__ uint32_t* seg(int e) const { return ctl + kStCtlWords + 4 * (int64_t)e; }
+    __device__ uint64_t* q() const { return reinterpret_cast<uint64_t*>(ctl + kStCtlWords + 4 * (int64_t)n); }
+};
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+    typedef __attribute__((address_space(1))) const uint32_t gU;
+    return __hip_atomic_load((gU*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t atomic_add_u32(uint32_t* p, uint32_t v) {
+    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // The scans of the fused launch, a separate (not inlined) function: its
 // registers are allocated apart from the walk's, so the walk keeps its three
 // waves per SIMD.  `lds` is the wave's LDS block (the walk's, dead by now).
@@ -1606,8 +1699,8 @@ __device__ __forceinline__ void fused_scans(const EpArrays ep, const sgmm_env_pa
     typedef __attribute__((address_space(3))) int lds_i32;
     const ScanShared<kFusedScanNT> sh{(double*)(lds_f64*)lds, (SL*)(lds_sl*)(lds + kFusedSel),
                                       (uint8_t*)(lds + kFusedSel + sizeof(SL)),
-                                      (uint32_t*)(lds_u32*)(lds + kFusedSel + sizeof(SL) + kFrontierSlots),
-                                      (int*)(lds_i32*)(lds + kFusedSel + sizeof(SL) + 5 * kFrontierSlots),
+                                      (uint32_t*)(lds_u32*)(lds + kFusedSel + sizeof(SL) + kFrontierRecs),
+                                      (int*)(lds_i32*)(lds + kFusedSel + sizeof(SL) + 5 * kFrontierRecs),
                                       (unsigned char*)lds};
     const int lane = threadIdx.x;
     uint32_t* started = fq.ctl + 32 * kXcds;
@@ -1701,11 +1794,28 @@ __device__ __forceinline__ void fused_scans(const EpArrays ep, const sgmm_env_pa
 #endif
 }
 
+// The frontier kernel's arguments, one struct: a wave walks several items
+// (its walk, then handed-over segments), and each walk reads them afresh
+// through a laundered kernarg pointer -- otherwise the compiler keeps every
+// argument the walk's prologue uses live through the tick loop for the next
+// item (80 SGPRs spilled)
+struct FrontierArgs {
+    sgmm_ticks tk;
+    EpArrays ep;
+    const sgmm_env_params* params;
+    GenomeSrc src;
+    int32_t inv_min, nsi;
+    uint64_t* cmaps;
+    uint32_t* ctr32;
+    uint32_t* kinfo;
+    double* rew;
+    FrontierQueue fq;
+    FrontierSteal fs;
+};
+typedef __attribute__((address_space(4))) const FrontierArgs kFrontierArgsK;
+
 template <int H, int NSI, bool FUSED>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(
-    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
-    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ cmaps, uint32_t* __restrict__ ctr32,
-    uint32_t* __restrict__ kinfo, double* __restrict__ rew, FrontierQueue fq) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16, KS = H / 4;
@@ -1717,9 +1827,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     constexpr int kWalkBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
     constexpr int kBig = (FUSED && kFusedScanLds > kWalkBig) ? kFusedScanLds : kWalkBig;
     __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
+    const FrontierQueue& fq = args.fq;
+    const FrontierSteal& fs = args.fs;
     if constexpr (FUSED) {
         if ((int)blockIdx.x >= fq.nwalk) {  // a scanner
-            fused_scans<NSI, false>(ep, params, inv_min, cmaps, ctr32, kinfo, rew, fq, (lds_u8*)big);
+            fused_scans<NSI, false>(args.ep, args.params, args.inv_min, args.cmaps, args.ctr32, args.kinfo, args.rew,
+                                    fq, (lds_u8*)big);
             return;
         }
         if (threadIdx.x == 0)
@@ -1728,11 +1841,19 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // wave b: the whole episode at order position b (b < fwhole), else chunk
     // group g of a split episode (two waves each, longest episodes first)
     const int b = (int)blockIdx.x;
-    const int pos = b < ep.fwhole ? b : ep.fwhole + ((b - ep.fwhole) >> 1);
-    const int nw = b < ep.fwhole ? 1 : 2, cg = b < ep.fwhole ? 0 : (b - ep.fwhole) & 1;
-    const int e = ep.order ? ep.order[pos] : pos;
-    if (!FUSED && cg == 0 && threadIdx.x == 0) ep.fnw[e] = (uint32_t)nw;  // fused: the queue entry carries it
-    const int32_t T = ep.len[e];
+    const int fwhole = args.ep.fwhole;
+    const int pos = b < fwhole ? b : fwhole + ((b - fwhole) >> 1);
+    const int nw0 = b < fwhole ? 1 : 2, cg0 = b < fwhole ? 0 : (b - fwhole) & 1;
+    const int e0 = args.ep.order ? args.ep.order[pos] : pos;
+    if (cg0 == 0 && threadIdx.x == 0) {
+        if (!FUSED) args.ep.fnw[e0] = (uint32_t)nw0;  // fused: the queue entry carries it
+        // one tick segment so far (before any hand-off's add to the same word)
+        if (!FUSED && fs.on)
+            __hip_atomic_exchange(fs.seg(e0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the last workgroup of the grid has started (so, dispatched in order, have
+    // all the walks): ctl[kStStarted]; ctl[kStActive] starts at the walk count
+    if (!FUSED && fs.on && threadIdx.x == 0 && b == (int)gridDim.x - 1) st_sc1(fs.ctl + kStStarted, 1u);
 
     // (13 200 bytes of LDS per wave for H = 32 with `big`: twelve waves fit a
     // CU's 160 KiB in 512-byte granules, the walks and the scanners of a
@@ -1743,13 +1864,30 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
     // successor (bits 9-11) and the fill (bit 12) written back by the column
     __shared__ uint16_t pl[kWave * (NSI - 1)];
+    __shared__ uint32_t st_ctx[5];  // hand-offs: episode, control pointer, episode count
 
-    auto walk = [&]() {  // the episode's walk (returns early past its last chunk)
+    // walk chunk group cg of episode e over chunk offsets [ub, ue) (ue < 0: the
+    // chunk length) as tick segment kseg; can_split: may hand ticks over
+    auto walk = [&](const FrontierArgs& A, const int e, const int nw, const int cg, const int kseg, const int ub,
+                    int ue, const bool can_split) {  // (returns early past its last chunk)
+    const sgmm_ticks& tk = A.tk;
+    const EpArrays& ep = A.ep;
+    const sgmm_env_params* __restrict__ params = A.params;
+    const GenomeSrc& src = A.src;
+    const int32_t inv_min = A.inv_min, nsi = A.nsi;
+    uint64_t* __restrict__ cmaps = A.cmaps;
+    uint32_t* __restrict__ ctr32 = A.ctr32;
+    uint32_t* __restrict__ kinfo = A.kinfo;
+    double* __restrict__ rew = A.rew;
+    const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
     const int CL = frontier_len(T, nw);
+    if (ue < 0) ue = CL;
     const int nch = (T + CL - 1) / CL;
     if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
-    const int lane = threadIdx.x, grp = lane >> 4, col = lane & 15;
+    int lane_ = (int)threadIdx.x;
+    asm volatile("" : "+v"(lane_));  // per item: lane-derived addresses are not kept live across items
+    const int lane = lane_, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
     const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
@@ -1781,7 +1919,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // per-lane path bookkeeping: byte s of cur = the state of the path that
     // started the chunk in state s (tracked starts: bits of sset)
     const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t sset = c >= nch ? 0u : ((c == 0 && ub == 0) ? 1u << (uint32_t)(-inv_min) : all);
     const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
     uint64_t cur = kIdentityMap;
     // trade count along the path from each tracked start: 16 bits per start,
@@ -1790,7 +1928,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
     for (int s = 0; s < (NSI + 1) / 2; ++s) cnt[s] = 0;
     bool merged = __builtin_popcount(sset) <= 1;
-    int kc = merged ? 0 : CL;
+    int kc = merged ? ub : CL;  // merge offset (CL: not within the segment)
     auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
 #ifdef SGMM_STAMPS
     // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
@@ -1807,10 +1945,60 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
     SGMM_FT(fs_t0);
 #endif
-    int64_t ti = tick_of(0);
+    int64_t ti = tick_of(ub);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
+    // hand-off checks at 1/2, 5/8 and 3/4 of the segment: each reads one global
+    // word (every walk polling it every few ticks made it a hot spot that cost
+    // the walks a third of their speed); the tail's walks are past half-way
+    // when the first helpers appear
+    const int chk_step = max(4, ((ue - ub) >> 3) & ~3);
+    const int chk_max = (int)A.fs.nchk;  // checks per segment
+    int next_chk = can_split ? ub + (((ue - ub) >> 1) & ~3) : INT_MAX, nchk = 0;
+    // what a hand-off needs, parked in LDS (not held in registers through the loop)
+    if (threadIdx.x == 0) {
+        st_ctx[0] = (uint32_t)e;
+        st_ctx[1] = (uint32_t)reinterpret_cast<uint64_t>(A.fs.ctl);
+        st_ctx[2] = (uint32_t)(reinterpret_cast<uint64_t>(A.fs.ctl) >> 32);
+        st_ctx[3] = (uint32_t)A.fs.n | ((uint32_t)A.fs.maxseg << 28);
+        st_ctx[4] = (uint32_t)A.fs.nchk;
+    }
 #pragma unroll 1
-    for (int tt = 0; tt < CL; ++tt) {
+    for (int tt = ub; tt < ue; ++tt) {
+        if (tt == next_chk) {
+            next_chk = ++nchk < chk_max ? next_chk + chk_step : INT_MAX;
+            // a helper waits and >= kStealMinRem ticks are left: the second
+            // half of them (from a multiple of 4, so a scan thread's ticks stay
+            // in one segment) becomes a new segment on the queue
+            const uint32_t idle = (uint32_t)__builtin_amdgcn_readfirstlane(
+                (int)ld_sc1_u32(reinterpret_cast<uint32_t*>((uint64_t)st_ctx[1] | ((uint64_t)st_ctx[2] << 32)) + kStIdle));
+            if ((int)idle > 0 && ue - tt >= kStealMinRem) {
+                const int m = tt + (((ue - tt) >> 1) & ~3);
+                int ok = 0;
+                if (threadIdx.x == 0) {
+                    const uint32_t ce = st_ctx[0];
+                    FrontierSteal f{reinterpret_cast<uint32_t*>((uint64_t)st_ctx[1] | ((uint64_t)st_ctx[2] << 32)), 1, 0,
+                                    (int32_t)(st_ctx[3] & 0x0FFFFFFFu), (int32_t)(st_ctx[3] >> 28), 0, 0};
+                    uint32_t* sg = f.seg((int)ce);
+                    // reserve a waiting helper (the read above may be stale)
+                    const int avail = (int)atomic_add_u32(f.ctl + kStIdle, 0xFFFFFFFFu);
+                    const uint32_t kk = avail >= 1 ? atomic_add_u32(sg, 1u) : 0xFFFFu;
+                    if (avail >= 1 && kk < (uint32_t)f.maxseg) {
+                        st_sc1(sg + kk, (uint32_t)m);
+                        atomic_add_u32(f.ctl + kStActive, 1u);
+                        const uint32_t slot = atomic_add_u32(f.ctl + kStTail, 1u);
+                        __hip_atomic_exchange(f.q() + slot,
+                                              (uint64_t)(ce + 1) | ((uint64_t)kk << 28) | ((uint64_t)m << 32) |
+                                                  ((uint64_t)ue << 48),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok = 1;
+                    } else {
+                        atomic_add_u32(f.ctl + kStIdle, 1u);  // give the reservation back
+                        if (avail >= 1) atomic_add_u32(f.ctl + kStNoSlot, 1u);
+                    }
+                }
+                if (__builtin_amdgcn_readfirstlane(ok)) ue = m;
+            }
+        }
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_a);
 #endif
@@ -2181,34 +2369,130 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = (int64_t)e * kFrontierSlots + c;
+        const int64_t ci = (int64_t)e * kFrontierRecs + kseg * kFrontierLanes + c;
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
         kinfo[ci] = (uint32_t)kc | (p0 << 29);
     }
     };
-    walk();
-    if constexpr (FUSED) {
-        const int lane = threadIdx.x;
-        // publish on this XCD's queue: the wave's stores drained into the L2,
-        // then one lane's atomics (every episode is one wave here); the push
-        // completes before the walk counts as finished
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-            const uint32_t x = xcc_id();
-            const uint32_t slot = (uint32_t)__hip_atomic_fetch_add(queue_state(fq, x), (uint64_t)1, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_exchange(&fq.q[(int64_t)x * fq.n + slot], (uint32_t)(e + 1), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+    // the launch's own walk, then (hand-offs on) the segments handed over to this wave
+    int w_e = e0, w_nw = nw0, w_cg = cg0, w_k = 0, w_ub = 0, w_ue = -1;
+    int registered = 0;  // lane 0: counted among the waiting helpers
+    int helper = 0;      // this wave's own walk is done
+#ifdef SGMM_STAMPS
+    // hand-off timeline (rows 49152 + b): start, own walk's end, exit, items walked, XCC
+    unsigned long long hs_t0, hs_t1 = 0, hs_n = 0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(hs_t0)::"memory");
+#endif
+#pragma unroll 1
+    while (true) {
+        const kFrontierArgsK* ka = (const kFrontierArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));  // re-read per item (see FrontierArgs)
+        walk(*(const FrontierArgs*)ka, w_e, w_nw, w_cg, w_k, w_ub, w_ue,
+             !FUSED && fs.on && w_nw == 1);
+        if constexpr (FUSED) {
+            const int e = e0;
+            const int lane = threadIdx.x;
+            // publish on this XCD's queue: the wave's stores drained into the L2,
+            // then one lane's atomics (every episode is one wave here); the push
+            // completes before the walk counts as finished
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const uint32_t fin = __hip_atomic_fetch_add(fq.ctl + 32 * kXcds + 32, 1u, __ATOMIC_RELAXED,
-                                                        __HIP_MEMORY_SCOPE_AGENT);
-            if (fin + 1 == (uint32_t)fq.nwalk)  // the last walk: every push is done, tell the scanners
-                for (uint32_t y = 0; y < (uint32_t)kXcds; ++y)
-                    __hip_atomic_fetch_add(queue_state(fq, y), 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0) {
+                const uint32_t x = xcc_id();
+                const uint32_t slot = (uint32_t)__hip_atomic_fetch_add(queue_state(fq, x), (uint64_t)1, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_exchange(&fq.q[(int64_t)x * fq.n + slot], (uint32_t)(e + 1), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t fin = __hip_atomic_fetch_add(fq.ctl + 32 * kXcds + 32, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                if (fin + 1 == (uint32_t)fq.nwalk)  // the last walk: every push is done, tell the scanners
+                    for (uint32_t y = 0; y < (uint32_t)kXcds; ++y)
+                        __hip_atomic_fetch_add(queue_state(fq, y), 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
         }
+        if (!fs.on) break;
+        // helper: walk handed-over segments until none is queued and no walk or
+        // segment is still running (every wave reaches that exit: items only
+        // come from running ones, and a walk's own hand-offs are on the queue
+        // before it finishes)
+        const int lane = threadIdx.x;
+        int got = -1, quit = 0;
+#ifdef SGMM_STAMPS
+        ++hs_n;
+        if (!helper) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(hs_t1)::"memory");
+#endif
+        if (lane == 0) {
+            atomic_add_u32(fs.ctl + kStActive, 0xFFFFFFFFu);  // this item is done
+            if (!helper) {  // this wave's own walk: stay as a helper?
+                if (b % fs.helper_every != 0) {
+                    quit = 1;  // one wave in helper_every stays
+                } else if (ld_sc1_u32(fs.ctl + kStStarted) == 0u) {
+                    quit = 1;  // walks may still wait for a wave slot: leave this one to them
+                    atomic_add_u32(fs.ctl + kStQuitEarly, 1u);
+                }
+            }
+        }
+        helper = 1;
+        quit = __builtin_amdgcn_readfirstlane(quit);
+#pragma unroll 1
+        while (!quit) {
+            if (lane == 0) {
+                // a few hundred helpers at most, each polling every ~7 us with
+                // read-modify-writes (loads could return stale L2 copies)
+                uint32_t h = atomic_peek(fs.ctl + kStHead);
+                const uint32_t t = atomic_peek(fs.ctl + kStTail);
+                while (h < t) {
+                    if (__hip_atomic_compare_exchange_strong(fs.ctl + kStHead, &h, h + 1, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        got = (int)h;
+                        break;
+                    }
+                }
+                if (got >= 0) {
+                    registered = 0;  // its reservation was taken by the donor (or is taken later)
+                } else if (atomic_peek(fs.ctl + kStActive) == 0u &&
+                           atomic_peek(fs.ctl + kStHead) >= atomic_peek(fs.ctl + kStTail)) {
+                    quit = 1;
+                } else if (!registered) {
+                    atomic_add_u32(fs.ctl + kStIdle, 1u);
+                    registered = 1;
+                }
+            }
+            got = __builtin_amdgcn_readfirstlane(got);
+            if (got >= 0 || __builtin_amdgcn_readfirstlane(quit)) break;
+            __builtin_amdgcn_s_sleep(127);
+            __builtin_amdgcn_s_sleep(127);
+        }
+        if (got < 0) break;
+        uint64_t it = 0;
+        if (lane == 0) {  // its donor has taken the slot and is about to store it
+            while ((it = atomic_peek64(fs.q() + got)) == 0ull) __builtin_amdgcn_s_sleep(1);
+            __hip_atomic_store(fs.q() + got, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // clean slot
+        }
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)it);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(it >> 32));
+        w_e = (int)(lo & 0x0FFFFFFFu) - 1;
+        w_k = (int)(lo >> 28);
+        w_ub = (int)(hi & 0xFFFFu);
+        w_ue = (int)(hi >> 16);
+        w_nw = 1;
+        w_cg = 0;
+        __syncthreads();  // the previous walk's LDS is reused
     }
+#ifdef SGMM_STAMPS
+    if (!FUSED && fs.on && threadIdx.x == 0 && 49152 + b < kStampWaves) {
+        unsigned long long t2;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
+        g_tstamps[49152 + b][0] = hs_t0;
+        g_tstamps[49152 + b][1] = hs_t1;
+        g_tstamps[49152 + b][2] = t2;
+        g_tstamps[49152 + b][3] = hs_n;
+        g_tstamps[49152 + b][4] = xcc_id();
+    }
+#endif
 }
 
 // After the fused launch: scans any episode its scanners left (normally
@@ -2585,7 +2869,7 @@ static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + kFrontierP
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps, e->n), e->order, e->n, nullptr};
+                    e->param, rew_stride(e->total_steps, e->n), e->order, e->n, nullptr, nullptr};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -2630,19 +2914,22 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 //   e * 128 + c, then u32 kinfo[n * 128] and u32 waves[n] -- each episode's
 //   wave count; the sections are sized for both)
 static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
-static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierSlots; }
+static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierRecs; }  // chunk records
 static size_t ws_cmaps(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps), n_frontier_slots(n)) * sizeof(uint64_t));
 }
 static size_t ws_ctr(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps) * sizeof(uint64_t), n_frontier_slots(n) * 8 * sizeof(uint32_t)));
 }
-// u32 kinfo[n * 128] | u32 waves[n] | (256-aligned) the fused launch's queues:
+// u32 kinfo[n * 256] | u32 waves[n] | (256-aligned) the fused launch's queues:
 // u32 ctl[11][32] (head, tail per XCD; walks started; walks finished;
-// episodes scanned), u32 q[8][n] -- zeroed by the launch
-static size_t ws_kinfo_head(int32_t n) { return align256((n_frontier_slots(n) + n) * sizeof(uint32_t)); }
+// episodes scanned), u32 q[8][n] | (256-aligned) the hand-offs: control words
+// u32[160], segment tables u32[4 n], queue u64[3 n + 64] -- both zeroed by the
+// launch that uses them
+static size_t ws_kinfo_head(int32_t n) { return align256((n_frontier_slots(n) + (size_t)n) * sizeof(uint32_t)); }
 static size_t ws_queue(int32_t n) { return 4 * 32 * (kXcds + 3) + (size_t)4 * kXcds * n; }
-static size_t ws_kinfo(int32_t n) { return ws_kinfo_head(n) + align256(ws_queue(n)); }
+static size_t ws_steal(int32_t n) { return 4 * (size_t)kStCtlWords + 16 * (size_t)n + 8 * (3 * (size_t)n + 64); }
+static size_t ws_kinfo(int32_t n) { return ws_kinfo_head(n) + align256(ws_queue(n)) + align256(ws_steal(n)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 // The workspace of a batch with n_inventory inventory values, with or
@@ -2674,15 +2961,23 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
 // Frontier kernel or table: the frontier kernel does ~1/3 of the table's
 // matrix work but walks each episode serially (one wave per episode), so it
 // needs many episodes to fill the chip; it is also the only path for episodes
-// longer than kMaxLen.  SGMM_TABLE_PATH=frontier / table forces either.
-constexpr int kFrontierMinEps = 2048;
+// longer than kMaxLen.  SGMM_TABLE_PATH=frontier / table forces either,
+// SGMM_FRONTIER_MIN_EPS moves the threshold.  Measured crossover (one rank's
+// shard of config 5, H = 32, 3600 ticks, per generation, profiles/r03_c5_shard*):
+// 256 episodes table 235 / frontier 363 us, 512: 365 / 435, 1024: 633 / 525,
+// 2048: 1078 / 572 -- the lines cross near 700 episodes.
+constexpr int kFrontierMinEps = 768;
 static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     if (arl || (hidden != 16 && hidden != 32)) return false;
     if (eps->max_len > kMaxLen) return true;
     const char* v = std::getenv("SGMM_TABLE_PATH");
     if (v && std::strcmp(v, "frontier") == 0) return true;
     if (v && *v) return false;
-    return eps->n >= kFrontierMinEps;
+    static const int min_eps = [] {
+        const char* m = std::getenv("SGMM_FRONTIER_MIN_EPS");
+        return m && std::atoi(m) > 0 ? std::atoi(m) : kFrontierMinEps;
+    }();
+    return eps->n >= min_eps;
 }
 
 // How many episodes run as one wave in the frontier kernel (the longest
@@ -2714,6 +3009,15 @@ static int simd_count() {
 // walks' tail slow those walks, and the last walks' scans still follow them.
 static bool frontier_fused() {
     const char* v = std::getenv("SGMM_FRONTIER_FUSED");
+    return v && std::strcmp(v, "1") == 0;
+}
+// SGMM_FRONTIER_STEAL=1: tick hand-offs between frontier walks (FrontierSteal).
+// Opt-in: bit-exact (tests/test_gpu_frontier.py) but no faster on config 3
+// (DESIGN.md section 5.1): the walks of the tail are past their hand-off
+// checks when the first helpers appear, and more helpers or checks make their
+// polling of the shared words cost more than the hand-offs save.
+static bool frontier_steal() {
+    const char* v = std::getenv("SGMM_FRONTIER_STEAL");
     return v && std::strcmp(v, "1") == 0;
 }
 static int32_t frontier_whole(int32_t n) {
@@ -2899,14 +3203,29 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
             fq = FrontierQueue{ctl, ctl + 32 * (kXcds + 3), fitness, trades, step, eps->n, nwalk, poll};
             SGMM_HIP(hipMemsetAsync(ctl, 0, ws_queue(eps->n), s));
         }
+        FrontierSteal fs{};
+        if (!fused && frontier_steal() && ep.fwhole > 0 && eps->n < (1 << 27)) {
+            uint32_t* ctl = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(kinfo) + ws_kinfo_head(eps->n) +
+                                                        align256(ws_queue(eps->n)));
+            const char* ms = std::getenv("SGMM_STEAL_MAXSEG");
+            const int maxseg = ms ? std::max(1, std::min(kFrontierSegs, std::atoi(ms))) : kFrontierSegs;
+            const char* ev = std::getenv("SGMM_STEAL_EVERY");
+            const char* nc = std::getenv("SGMM_STEAL_CHK");
+            const int every = ev && std::atoi(ev) > 0 ? std::atoi(ev)
+                                                      : std::max(1, nwalk / std::max(1, simd_count() / 4));  // ~1 per CU
+            fs = FrontierSteal{ctl, 1, nwalk, eps->n, maxseg, every, nc && std::atoi(nc) > 0 ? std::atoi(nc) : 3};
+            SGMM_HIP(hipMemsetAsync(ctl, 0, ws_steal(eps->n), s));
+            SGMM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctl + kStActive), nwalk, 1, s));
+            ep.fseg = ctl + kStCtlWords;  // the scan's segment tables
+        }
+        const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
+                              kinfo, rew, fq, fs};
 #define SGMM_FRONTIER(H_, NSI_)                                                                              \
     do {                                                                                                     \
         if (fused)                                                                                           \
-            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, true>), grid, block, 0, s, *ticks, ep, params, src,     \
-                        eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);          \
+            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, true>), grid, block, 0, s, fa);                         \
         else                                                                                                 \
-            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false>), grid, block, 0, s, *ticks, ep, params, src,    \
-                        eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);          \
+            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false>), grid, block, 0, s, fa);                        \
     } while (0)
         if (hidden == 16) {
             if (nsi <= 5) SGMM_FRONTIER(16, 5);

@@ -67,11 +67,13 @@ def test_argument_errors_need_no_gpu(sgmm):
         assert rc == -1 and b"genome too large" in L.sgmm_last_error()
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
-    # frontier kernel (128 chunk slots per episode: u64 map, u32[8] counts, u32 merge info;
-    # u32 wave count per episode; then the fused launch's queues: 11 x 128 B of counters + u32
-    # q[8][n], 256-aligned) (planes: 1000 ticks + 528 padding rows per episode of the frontier
-    # layout -- 128-byte aligned episode blocks -- rounded to 32)
-    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 128 * 8 + 4 * 128 * 32 + 2304 + 1536
+    # frontier kernel (256 chunk records per episode -- 64 chunks x 4 tick segments: u64 map,
+    # u32[8] counts, u32 merge info; u32 wave count per episode; then
+    # the fused launch's queues: 11 x 128 B of counters + u32 q[8][n], 256-aligned; then the
+    # hand-off counters u32[160] + segment tables u32[4 n] + queue u64[3 n + 64], 256-aligned) (planes: 1000 ticks + 528
+    # padding rows per episode of the frontier layout -- 128-byte aligned episode blocks --
+    # rounded to 32)
+    assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 256 * 8 + 4 * 256 * 32 + 4352 + 1536 + 1536
                                                          + 5 * 3136 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000

@@ -89,13 +89,33 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
 
 @pytest.mark.parametrize("nw", ["", "1", "2", "3"], ids=["default", "1wave", "2waves", "balanced"])
 def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
-    """From 2048 episodes on the frontier kernel is the default: 2100 ragged
+    """From 768 episodes on the frontier kernel is the default: 2100 ragged
     episodes bit-exact against the oracle (balanced: 972 of them split into
     two waves, the rest whole, in one launch)."""
     if nw:
         monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
     lens = 300 + (np.arange(2100) * 37) % 900
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=47, sigma=0.3)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
+def test_frontier_default_selection_config5_shard(sgmm, oracle):
+    """One rank's shard of BASELINE config 5 on 8 GPUs: 2 x 512 individuals =
+    1024 episodes of 3600 ticks, H = 32.  The measured table / frontier
+    crossover lies between 512 and 1024 episodes (profiles/r03_c5_shard*), so
+    the default selection runs the frontier kernel here; bit-exact against the
+    oracle."""
+    from sgmm_amd import _lib
+    lens = 3600 - (np.arange(1024) % 5) * 4
+    _lib.profile_read()
+    _lib.profile_enable(True)
+    try:
+        fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=53, sigma=0.1)
+        kernels = _lib.profile_read()
+    finally:
+        _lib.profile_enable(False)
+    assert "policy_frontier" in kernels, kernels
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
 
@@ -180,3 +200,57 @@ def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=51, sigma=0.3)
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
+
+
+def test_frontier_tick_handoffs_equal_whole(sgmm, oracle, monkeypatch):
+    """Tick hand-offs (SGMM_FRONTIER_STEAL=1, opt-in): a walk that sees a
+    waiting helper hands the second half of its remaining ticks over as a new
+    segment of its chunks (every start state tracked), so the episode's
+    records come in up to 4 segments that the scan chains in tick order.  On
+    a batch big enough to have helpers (2560 episodes; every finished wave a
+    helper, eight checks per segment) the results equal the walks without
+    hand-offs bit for bit, and hand-offs did happen."""
+    from sgmm_amd import synthetic
+    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
+    monkeypatch.setenv("SGMM_FRONTIER_NW", "1")
+    monkeypatch.setenv("SGMM_FRONTIER_FUSED", "0")
+    P, T, H = 2560, 4560, 32  # 72-tick chunks: a half-way check leaves >= 16 ticks
+    b = synthetic.bundle_510300(T, seed=41)
+    st = synthetic.train_stats(b)
+    # a spread of sigmas: policies that rarely fill keep their paths apart (heavy walks)
+    pop = torch.cat([synthetic.population(P // 4, H, sigma=s, seed=42 + k)
+                     for k, s in enumerate((0.05, 0.2, 0.5, 1.0))])
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.001, tick_size=0.001)], DEV)
+    lens = np.full(P, T)
+    lens[::7] = T - 124  # ragged lengths
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P)).to(DEV)
+    eng = sgmm.RolloutEngine(DEV)
+    mm = pop.to(DEV)
+    monkeypatch.setenv("SGMM_FRONTIER_STEAL", "0")
+    f0, t0 = (x.cpu().numpy() for x in eng.fitness(ticks, eb, params, mm, H))
+    monkeypatch.setenv("SGMM_FRONTIER_STEAL", "1")
+    monkeypatch.setenv("SGMM_STEAL_EVERY", "1")
+    monkeypatch.setenv("SGMM_STEAL_CHK", "8")
+    f1, t1 = (x.cpu().numpy() for x in eng.fitness(ticks, eb, params, mm, H))
+    torch.cuda.synchronize()
+    # the segment tables (workspace layout of sgmm_rollout_workspace_bytes: chunk maps,
+    # trade counts, merge info + wave counts, the fused queues, then the hand-off area)
+    def a256(x):
+        return (x + 255) & ~255
+    n, steps = P, int(lens.sum())
+    nchunk = steps // 64 + n + 1
+    off = a256(max(nchunk, n * 256) * 8) + a256(max(nchunk * 8, n * 256 * 32)) + a256((n * 256 + n) * 4) + \
+        a256(4 * 32 * 11 + 4 * 8 * n)
+    segs = eng._ws[off + 640:off + 640 + 16 * n].view(torch.int32).cpu().numpy().reshape(n, 4)[:, 0]
+    assert (segs > 1).sum() > 0, "no hand-off happened"
+    assert np.array_equal(t0, t1) and np.array_equal(f0, f1)
+    # and the first episodes against the oracle
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    k = 48
+    wf, wt = oracle.evaluate_batch(pop[:k].numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(k), None,
+                                   np.zeros(k), lens[:k], np.zeros(k), [oracle.params(phi=0.001, tick=0.001)],
+                                   n_threads=8)
+    assert np.array_equal(wt, t1[:k]) and np.array_equal(wf, f1[:k])
