@@ -82,7 +82,8 @@ def parse():
                          "(0: all of them)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-episodes", type=int, default=64, help="episodes in the CPU-baseline sample")
+    ap.add_argument("--cpu-episodes", type=int, default=256,
+                    help="episodes in the CPU-baseline sample (256 x 4560 ticks: ~20 core-seconds on Pool(16))")
     ap.add_argument("--pmc", default="", help="PMC traffic summary JSON (default: newest for this config)")
     ap.add_argument("--shard-of", type=int, default=1,
                     help="strong-scaled configs (4, 5): run ONE rank's shard of an N-GPU run on this GPU "
