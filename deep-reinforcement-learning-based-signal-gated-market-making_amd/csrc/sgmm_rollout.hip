@@ -929,6 +929,19 @@ constexpr int kFrontierPad = 4 * kFrontierSlots + 16;  // plane rows per episode
 __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
     return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
 }
+// Within a group's block, the reward of chunk (lane) l at tick offset u: the
+// 64 chunks' 4-tick groups side by side -- a walk's store of one tick is one
+// coalesced 2 KB span (each 128-byte line complete after 4 ticks), a scan
+// thread's 4 ticks are 32 contiguous bytes (one cache line, two 16-byte loads
+// instead of four 8-byte loads on four lines).  SGMM_PLANE1: round 2's rows
+// (tick offset u, lane l at u * 64 + l).
+__host__ __device__ __forceinline__ int64_t frontier_row(int u, int l) {
+#ifdef SGMM_PLANE1
+    return (int64_t)u * kFrontierLanes + l;
+#else
+    return ((int64_t)(u >> 2) * kFrontierLanes + l) * 4 + (u & 3);
+#endif
+}
 
 // ------------------------------------------------------------------ exact ordered sum
 // The episode total is the reference's sequential float64 sum
@@ -1381,7 +1394,10 @@ struct ScanShared {
     unsigned char* tail;  // generation-tail scratch (aliases sel)
 };
 
-template <int NSM, int NT, bool FR, int TPB, bool SC1, bool TAIL = true>
+// SEG: the episode's chunks may be cut into tick segments (the hand-off
+// launch); without it the gather indexes chunk records directly (the segment
+// lookup cost the config-3 scan ~14 us)
+template <int NSM, int NT, bool FR, int TPB, bool SC1, bool TAIL = true, bool SEG = false>
 __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, const sgmm_env_params* __restrict__ params,
                                              int32_t inv_min, const uint64_t* __restrict__ cmaps,
                                              const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ kinfo,
@@ -1403,7 +1419,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     // the segments in tick order -- ord[j] = record block of the j-th, bnd[j] =
     // its first chunk offset (INT_MAX past the last); uniform
     int nseg = 1, ord[kFrontierSegs] = {0, 1, 2, 3}, bnd[kFrontierSegs] = {0, INT_MAX, INT_MAX, INT_MAX};
-    if (FR && nw == 1 && ep.fseg) {
+    if (FR && SEG && nw == 1 && ep.fseg) {
         nseg = (int)min((uint32_t)kFrontierSegs, ld_rec<SC1>(ep.fseg + 4 * (int64_t)e));
         for (int k = 1; k < nseg; ++k) bnd[k] = (int)ld_rec<SC1>(ep.fseg + 4 * (int64_t)e + k);
         for (int k = 1; k < nseg; ++k)  // insertion sort by offset (segment 0 starts at 0)
@@ -1416,7 +1432,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
             }
     }
     SGMM_STAMP(e, 0);
-    if (FR && nseg > 1) {  // one round (a whole episode has <= 64 chunks), per chunk its segments in order
+    if (FR && SEG && nseg > 1) {  // one round (a whole episode has <= 64 chunks), per chunk its segments in order
         if (tid < kWave) {
             const int c = lane;
             uint64_t mk[kFrontierSegs], M = kIdentityMap;
@@ -1494,10 +1510,11 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
                     const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
                     // the record of the segment holding offset u (segment offsets are
                     // multiples of kSumTpt: a thread's ticks lie in one segment)
-                    const int v = ord[(u >= bnd[1]) + (u >= bnd[2]) + (u >= bnd[3])] * kFrontierLanes + c;
+                    const int v = SEG ? ord[(u >= bnd[1]) + (u >= bnd[2]) + (u >= bnd[3])] * kFrontierLanes + c : c;
                     const uint32_t ki = kin[v];
                     const int kc = (int)(ki & 0x1FFFFFFFu);
                     const int64_t pst = start[v], pp0 = ki >> 29;
+#ifdef SGMM_PLANE1
                     const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        c % kFrontierLanes;
 #pragma unroll
@@ -1506,6 +1523,35 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
                         r[g][j] = ld_rec<SC1>(rew + (u + jj >= kc ? pp0 : pst) * ep.rs + rb +
                                               (int64_t)(u + jj) * kFrontierLanes);
                     }
+#else
+                    // the chunk's 4 ticks u .. u + 3 are 32 contiguous bytes (frontier_row)
+                    const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
+                                       frontier_row(u, c % kFrontierLanes);
+                    if constexpr (SC1) {
+#pragma unroll
+                        for (int j = 0; j < kSumTpt; ++j) {
+                            const int jj = min(j, n - 1 - i0);
+                            r[g][j] = ld_rec<true>(rew + (u + jj >= kc ? pp0 : pst) * ep.rs + rb + jj);
+                        }
+                    } else {
+                        // one plane for the 4 ticks unless the paths merge inside them
+                        double2 a0{0.0, 0.0}, a1{0.0, 0.0}, b0{0.0, 0.0}, b1{0.0, 0.0};
+                        if (u < kc) {
+                            const double2* pa = reinterpret_cast<const double2*>(rew + pst * ep.rs + rb);
+                            a0 = pa[0];
+                            a1 = pa[1];
+                        }
+                        if (u + kSumTpt - 1 >= kc) {
+                            const double2* pb = reinterpret_cast<const double2*>(rew + pp0 * ep.rs + rb);
+                            b0 = pb[0];
+                            b1 = pb[1];
+                        }
+                        r[g][0] = u >= kc ? b0.x : a0.x;
+                        r[g][1] = u + 1 >= kc ? b0.y : a0.y;
+                        r[g][2] = u + 2 >= kc ? b1.x : a1.x;
+                        r[g][3] = u + 3 >= kc ? b1.y : a1.y;
+                    }
+#endif
                 } else {
                     const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
 #pragma unroll
@@ -1564,7 +1610,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
 }
 
 // one workgroup per episode (the table path, and the frontier path unfused)
-template <int NSM, int NT, bool FR, int TPB = NT>
+template <int NSM, int NT, bool FR, int TPB = NT, bool SEG = false>
 __global__ __launch_bounds__(TPB) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
     const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
@@ -1572,12 +1618,12 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[FR ? kFrontierRecs : kMaxLen / kChunk];
-    __shared__ uint32_t kin[FR ? kFrontierRecs : 1];
+    __shared__ uint8_t start[FR ? (SEG ? kFrontierRecs : kFrontierSlots) : kMaxLen / kChunk];
+    __shared__ uint32_t kin[FR ? (SEG ? kFrontierRecs : kFrontierSlots) : 1];
     __shared__ int red_trades;
     const int e = blockIdx.x;
     const ScanShared<NT> sh{reinterpret_cast<double*>(lds), &L, start, kin, &red_trades, lds};
-    scan_episode<NSM, NT, FR, TPB, false>(e, FR ? (int)ep.fnw[e] : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew,
+    scan_episode<NSM, NT, FR, TPB, false, true, SEG>(e, FR ? (int)ep.fnw[e] : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew,
                                           fitness, trades_out, step, (int)gridDim.x, sh);
 }
 
@@ -1814,7 +1860,10 @@ struct FrontierArgs {
 };
 typedef __attribute__((address_space(4))) const FrontierArgs kFrontierArgsK;
 
-template <int H, int NSI, bool FUSED>
+// STEAL: the hand-off variant (a wave walks items in a loop; its prologue
+// spills a few registers outside the tick loop) -- the default launch is the
+// single-walk instantiation, with no loop and no spills
+template <int H, int NSI, bool FUSED, bool STEAL = false>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
@@ -1886,7 +1935,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     const int nch = (T + CL - 1) / CL;
     if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
     int lane_ = (int)threadIdx.x;
-    asm volatile("" : "+v"(lane_));  // per item: lane-derived addresses are not kept live across items
+    if constexpr (STEAL) asm volatile("" : "+v"(lane_));  // per item: lane-derived addresses not kept live across items
     const int lane = lane_, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
@@ -1953,9 +2002,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // when the first helpers appear
     const int chk_step = max(4, ((ue - ub) >> 3) & ~3);
     const int chk_max = (int)A.fs.nchk;  // checks per segment
-    int next_chk = can_split ? ub + (((ue - ub) >> 1) & ~3) : INT_MAX, nchk = 0;
+    int next_chk = (STEAL && can_split) ? ub + (((ue - ub) >> 1) & ~3) : INT_MAX, nchk = 0;
     // what a hand-off needs, parked in LDS (not held in registers through the loop)
-    if (threadIdx.x == 0) {
+    if (STEAL && threadIdx.x == 0) {
         st_ctx[0] = (uint32_t)e;
         st_ctx[1] = (uint32_t)reinterpret_cast<uint64_t>(A.fs.ctl);
         st_ctx[2] = (uint32_t)(reinterpret_cast<uint64_t>(A.fs.ctl) >> 32);
@@ -1964,7 +2013,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     }
 #pragma unroll 1
     for (int tt = ub; tt < ue; ++tt) {
-        if (tt == next_chk) {
+        if (STEAL && tt == next_chk) {
             next_chk = ++nchk < chk_max ? next_chk + chk_step : INT_MAX;
             // a helper waits and >= kStealMinRem ticks are left: the second
             // half of them (from a multiple of 4, so a scan thread's ticks stay
@@ -2299,12 +2348,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa);
             asm volatile("" : "+s"(pu));
             double* const prow = reinterpret_cast<double*>(pu);
-            const int64_t toff = (int64_t)tt * kFrontierLanes;
+            const int64_t toff = frontier_row(tt, 0);  // uniform; lane l at + frontier_row(0, l)
 #pragma unroll
             for (int s = 0; s < NSI; ++s) {
                 if (!((sset >> s) & 1u)) continue;
                 const uint32_t st = map_get(cur, (uint32_t)s);
-                if (!merged || (uint32_t)s == p0) prow[s * prs + toff + lane] = rl[st * kWave + lane];
+                if (!merged || (uint32_t)s == p0) prow[s * prs + toff + frontier_row(0, lane)] = rl[st * kWave + lane];
                 cnt[s >> 1] += ((trm >> st) & 1u) << (16 * (s & 1));
             }
             cur = map_then(cur, stepmap);
@@ -2390,7 +2439,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         const kFrontierArgsK* ka = (const kFrontierArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(ka));  // re-read per item (see FrontierArgs)
         walk(*(const FrontierArgs*)ka, w_e, w_nw, w_cg, w_k, w_ub, w_ue,
-             !FUSED && fs.on && w_nw == 1);
+             STEAL && !FUSED && fs.on && w_nw == 1);
         if constexpr (FUSED) {
             const int e = e0;
             const int lane = threadIdx.x;
@@ -2413,7 +2462,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
             }
             break;
         }
-        if (!fs.on) break;
+        if (!STEAL || !fs.on) break;
         // helper: walk handed-over segments until none is queued and no walk or
         // segment is still running (every wave reaches that exit: items only
         // come from running ones, and a walk's own hand-offs are on the queue
@@ -3118,23 +3167,37 @@ static int scan_threads(int64_t n) {
     return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : kWave);
 }
 
+template <int NSM, bool FR, bool SEG = false>
+static void launch_path_scan_t(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
+                             const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
+                             const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
+                             int32_t* trades, const StepArgs& step) {
+    if (nt == kWave)
+        SGMM_LAUNCH((k_path_scan<NSM, 4 * kWave, FR, kWave, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, kinfo, rew, fitness, trades, step);
+    else if (nt == kScanThreads)
+        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR, kScanThreads, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, kinfo, rew, fitness, trades, step);
+    else if (nt == 512)
+        SGMM_LAUNCH((k_path_scan<NSM, 512, FR, 512, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    kinfo, rew, fitness, trades, step);
+    else
+        SGMM_LAUNCH((k_path_scan<NSM, 256, FR, 256, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
+                    kinfo, rew, fitness, trades, step);
+}
+
+// the frontier scan with segmented chunks only for the hand-off launch (ep.fseg set)
 template <int NSM, bool FR>
 static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
                              const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
                              const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
                              int32_t* trades, const StepArgs& step) {
-    if (nt == kWave)
-        SGMM_LAUNCH((k_path_scan<NSM, 4 * kWave, FR, kWave>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
-                    cmaps, ctr, kinfo, rew, fitness, trades, step);
-    else if (nt == kScanThreads)
-        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
-                    cmaps, ctr, kinfo, rew, fitness, trades, step);
-    else if (nt == 512)
-        SGMM_LAUNCH((k_path_scan<NSM, 512, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    kinfo, rew, fitness, trades, step);
+    if (FR && ep.fseg)
+        launch_path_scan_t<NSM, true, true>(nt, n, lds, s, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness,
+                                            trades, step);
     else
-        SGMM_LAUNCH((k_path_scan<NSM, 256, FR>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    kinfo, rew, fitness, trades, step);
+        launch_path_scan_t<NSM, FR>(nt, n, lds, s, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness, trades,
+                                    step);
 }
 
 // table + path scan (+ the generation tail when step.st) for one batch
@@ -3224,6 +3287,8 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     do {                                                                                                     \
         if (fused)                                                                                           \
             SGMM_LAUNCH((k_policy_frontier<H_, NSI_, true>), grid, block, 0, s, fa);                         \
+        else if (fs.on)                                                                                      \
+            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false, true>), grid, block, 0, s, fa);                  \
         else                                                                                                 \
             SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false>), grid, block, 0, s, fa);                        \
     } while (0)
