@@ -29,6 +29,10 @@ Workloads (--config, BASELINE.json configs; synthetic SURVEY 8d ticks):
   5            two assets (510300: tick 0.001, phi 1e-4; 688981: tick 0.01,
                phi 1e-2) x population 4096, H=32, 3600 + 720 ticks; each
                population split over the N ranks (strong).
+  6, 7         not BASELINE configs: the shape the reference's own pipeline
+               trains (pipeline/agent_trainer.py:136-137: DRLEngine(pop_size=50),
+               H=32, ~15 training days = 3600 ticks + 720 validation ticks),
+               phi 1e-4 on 510300 ticks; 7 with the adversary (USE_ARL).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config C]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -64,7 +68,10 @@ CONFIGS = {
     4: dict(pops=[(0.0001, 0.001, "510300")], P=256, H=32, T=3600, Tv=720, arl=True, scaling="strong"),
     5: dict(pops=[(0.0001, 0.001, "510300"), (0.01, 0.01, "688981")], P=4096, H=32, T=3600, Tv=720,
             arl=False, scaling="strong"),
+    6: dict(pops=[(0.0001, 0.001, "510300")], P=50, H=32, T=3600, Tv=720, arl=False, scaling="weak"),
+    7: dict(pops=[(0.0001, 0.001, "510300")], P=50, H=32, T=3600, Tv=720, arl=True, scaling="weak"),
 }
+BASELINE_CONFIGS = (2, 3, 4, 5)
 
 
 def parse():
@@ -131,7 +138,10 @@ def describe(spec, world, P_glob, best_val):
     cfg_match = {k: v for k, v in CONFIGS.items()
                  if (v["P"], v["H"], v["T"], v["Tv"], v["pops"], v["arl"]) ==
                  (spec["P"], H, spec["T"], spec["Tv"], pops, spec["arl"])}
-    head = f"BASELINE config {next(iter(cfg_match))}: " if cfg_match else "custom (not a BASELINE config): "
+    c = next(iter(cfg_match), None)
+    head = (f"BASELINE config {c}: " if c in BASELINE_CONFIGS else
+            "the reference pipeline's training shape (agent_trainer.py:136-137, not a BASELINE config): "
+            if c is not None else "custom (not a BASELINE config): ")
     lam = ", ".join(f"phi={p} tick={t} {a}" for p, t, a in pops)
     return (head + f"{len(pops)} GA population(s) x {P_glob} individuals ({lam}), "
             f"TradingPolicy 3->{H}->{H}->2{' + AdversaryPolicy pairs' if spec['arl'] else ''}, synthetic ticks "
@@ -329,8 +339,7 @@ def main():
     # the training launch: training episodes (+ every validation episode when fused)
     steps_per_launch = K * n_rank * (T if best_val else T + Tv)
     fl = flop_per_step(H)
-    kname = next((k for k in ("policy_frontier_scan", "policy_frontier", "policy_table") if k in kernels),
-                 "policy_table")
+    kname = next((k for k in ("policy_frontier", "policy_table") if k in kernels), "policy_table")
     tab = kernels.get(kname)
     pmc = latest_pmc(args.pmc, args.config)
     roofline = None
@@ -343,12 +352,9 @@ def main():
                 + ("training" if best_val else "training + validation") + " ticks of one launch). "
                 + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.2-1.35 per "
                    "training tick on this workload, in 16-lane MFMA tiles)" if kname.startswith("policy_frontier") else
-                   "k_policy_table_v3 evaluates every inventory state (5x this work)")
-                + ("; the launch also runs every episode's path scan and the GA tell (fused: the time is walk + "
-                   "scan + tell)" if kname == "policy_frontier_scan" else ""))
+                   "k_policy_table_v3 evaluates every inventory state (5x this work)"))
         roofline = {"bound": "mfma", "pipe": "fp32 (gfx950 f32 MFMA peak == f32 VALU peak)",
-                    "kernel": ("k_policy_frontier<fused scans>" if kname == "policy_frontier_scan" else
-                               "k_policy_frontier" if kname == "policy_frontier" else
+                    "kernel": ("k_policy_frontier" if kname == "policy_frontier" else
                                "k_policy_table_mfma (adversary)" if spec["arl"] else "k_policy_table_v3"),
                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
@@ -365,14 +371,18 @@ def main():
     if rank == 0:
         gens_per_s = args.steps / dt
         out = {
-            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world,
+            # a shard line is ONE rank's share of a strong-scaled run: its own metric
+            # name and config id, so it cannot be taken for the whole config
+            "metric": METRIC if shard_of == 1 else f"{METRIC} [one rank's shard: 1 of {shard_of}]",
+            "value": value, "unit": "env-steps/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
             "higher_is_better": True, "scaling": spec["scaling"], "vs_baseline": None,
             "dtype": "f32+f64", "data": "synthetic",
             "config": {"workload": describe(spec, world, P_glob, best_val) + (
                            f"; ONE RANK'S SHARD: 1 of {shard_of} ranks (ceil(P/{shard_of}) = {P} individuals per "
                            f"population, rollout + tell on this GPU, no exchange)" if shard_of > 1 else ""),
-                       "config_id": args.config, "shard_of": shard_of,
+                       "config_id": args.config if shard_of == 1 else f"{args.config}/shard-1-of-{shard_of}",
+                       "shard_of": shard_of,
                        "populations": K, "population_global": P_glob, "population_per_gpu": n_rank,
                        "phis": [p for p, _, _ in spec["pops"]], "hidden": H, "ticks_train": T, "ticks_val": Tv,
                        "adversary": spec["arl"], "val_mode": "best" if best_val else "fused",

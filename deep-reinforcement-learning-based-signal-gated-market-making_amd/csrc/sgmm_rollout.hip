@@ -58,18 +58,11 @@ struct EpArrays {
     const int64_t* step_off;
     const int32_t* param;
     int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
-    const int32_t* order;  // frontier kernel: episode of workgroup b (NULL: b)
-    // frontier kernel: the episodes at order positions >= fwhole are split
-    // into two waves (two 64-chunk groups), the others run as one wave; the
-    // policy kernel records each episode's wave count in fnw[e] for the scan
-    int32_t fwhole;
-    uint32_t* fnw;
-    // frontier kernel, whole episodes: the chunks' tick ranges may be cut into
-    // up to kFrontierSegs segments walked by different waves (a walk hands the
-    // second half of its remaining ticks to an idle wave): fseg[4 e] = segments
-    // allocated (1 + hand-offs; >= kFrontierSegs when one was refused), fseg[4 e
-    // + k] = the chunk tick offset where segment k starts (segment 0 at 0)
-    uint32_t* fseg;
+    const int32_t* order;  // frontier kernel: episode of order position p (NULL: p)
+    // frontier kernel: every episode of the launch is cut into ngrp groups of
+    // 64 chunks, one wave each (chunks of frontier_len(T, ngrp) ticks); the
+    // path scan derives the same chunk layout from it
+    int32_t ngrp;
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -602,30 +595,21 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : ((ARL && H <= 32) ? 3 : 1)
 }
 
 // ------------------------------------------------------------------ table v3: one state per MFMA stream
-// Same outputs and arithmetic as k_policy_table_mfma (!ARL), re-scheduled so
-// the matrix pipe never waits for the vector work of the state before it.
-// Two accumulator sets alternate between the inventory states; region r
-// (one per state, fenced by sched_barrier) issues
-//   MFMA:  layer 1 + layer 2 of state r+1 into set (r+1)&1 (pure registers),
-//   VALU:  relu + LDS transpose of state r (set r&1), layer 3 of state r and
-//          its FPT step (fp64), the transition byte and the reward staging,
-// so one wave carries both pipes; the vector work of a region (~200 issue
-// slots) fits in the 64 MFMA gaps (24 free cycles each, MI355X_MICROARCH.md
-// cycle constants).  Every lane computes every state (padded lanes read a
-// clamped tick and are masked out of the maps afterwards), so a region is a
-// single basic block.  Packed f32 FMAs are avoided beside the MFMAs (a
-// v_pk_fma_f32 there costs ~22 cycles more than two v_fma_f32).
-// ARL (MODE 1 only): the adversary's state space (inventory x previous fill
-// flags, 4 nsi states): state si's policy outputs drive the FPT step from its
-// four flag states (adversary deltas from a per-episode LUT), each reward
-// goes straight to its per-state plane and the tick's 2-bit fill codes to
-// fills[row] -- k_policy_table_mfma's outputs.
-template <int H, int NSI, int MODE, bool ARL>
+// Same outputs and arithmetic as k_policy_table_mfma (no adversary),
+// re-scheduled: one accumulator set; per inventory state a vector block
+// (relu + LDS transpose of state si, layer 1 of si+1, layer 3 and the FPT step
+// of si) and a pure MFMA block (layer 2 of si+1).  f32 MFMAs and vector ops of
+// ONE wave do not overlap on gfx950 (tools/mb/mb_mfma_valu.hip), so the blocks
+// are kept apart and the overlap comes from the other waves of the SIMD.
+// Every lane computes every state (padded lanes read a clamped tick and are
+// masked out of the maps afterwards).  (Round 2's alternative with two
+// accumulator sets interleaved, "v3i", and this schedule for the adversary
+// table measured slower: tools/experiments/round3_opt_in_paths.patch.)
+template <int H, int NSI>
 __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k_policy_table_v3(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
     int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
-    uint64_t* __restrict__ fills, double* __restrict__ rew) {
-    static_assert(!ARL || MODE == 1, "adversary: the one-accumulator schedule");
+    double* __restrict__ rew) {
     static_assert(H % 16 == 0 && H <= 32, "v3 table: H = 16 or 32");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16;   // 16-neuron row tiles of layer 2
@@ -658,20 +642,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
     __shared__ __attribute__((aligned(16))) double rl_s[4][NSI][kWave];  // [state][lane] path-plane rewards
     static_assert(sizeof(rl_s) >= sizeof(float) * L::N, "genome fits the reward buffer");
     float* gsm = reinterpret_cast<float*>(&rl_s[0][0][0]);
-    __shared__ float gsa[ARL ? kAdvParams : 1];
-    __shared__ int32_t lut[2][ARL ? 32 : 1];  // adversary deltas (bid, ask) per state
-    const int ai = (ARL && ep.adv) ? ep.adv[e] : -1;
-    stage_genomes(src, e, ep.genome[e], ai, L::N, gsm, ARL ? gsa : nullptr);
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
     __syncthreads();
-    if constexpr (ARL) {
-        if ((int)threadIdx.x < 4 * nsi) {
-            const int st = threadIdx.x;
-            int32_t da = 0, db = 0;
-            if (ai >= 0) adv_delta(gsa, params[ep.param[e]], inv_min + (st >> 2), (st >> 1) & 1, st & 1, da, db);
-            lut[0][st] = da;
-            lut[1][st] = db;
-        }
-    }
     __shared__ __attribute__((aligned(16))) float w3i[2 * H];  // (W3[0][j], W3[1][j]) pairs
     if (threadIdx.x < 2 * H) w3i[threadIdx.x] = gsm[L::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
     const float* g = gsm;
@@ -711,33 +683,19 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
     float* hb = hb_s[wv];
     double* rl = &rl_s[wv][0][0];
 
-    f32x4 acc[MODE == 0 ? 2 : 1][4][NT];
+    f32x4 acc[4][NT];
     uint64_t map = kIdentityMap;
     uint32_t traded = 0;
-    uint64_t fw = 0;  // ARL: 2 fill bits per state
     const bool valid = t0 + lane < T;
     const int64_t row = ep.step_off[e] + t0 + lane;
-    auto layer12 = [&](int si, int b) {  // layer 1 (VALU) + layer 2 (MFMA) of state si into set b
-        const float x2 = (float)((double)(inv_min + si) / 2.0);
-#pragma unroll
-        for (int i = 0; i < KS; ++i)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float h1 = relu(__builtin_fmaf(w1s[i], x2, pre[q][i]));
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt)
-                    acc[b][q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1,
-                                                                         i == 0 ? b2c[rt] : acc[b][q][rt], 0, 0, 0);
-            }
-    };
-    auto transpose = [&](int b) {  // relu(H2) of set b -> LDS [sample][neuron]
+    auto transpose = [&]() {  // relu(H2) -> LDS [sample][neuron]
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int rt = 0; rt < NT; ++rt) {
                 f32x4 v;
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = relu(acc[b][q][rt][r]);
+                for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
                 *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
             }
     };
@@ -757,41 +715,14 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
         }
         const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
         const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-        if constexpr (ARL) {
-            if (si < nsi) {  // uniform
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const int st = 4 * si + c;
-                    const StepOut so = ftp_step(p, inv_min + si, oa + lut[0][st], ob + lut[1][st], tmid, task, tbid,
-                                                tbmax, tsmin);
-                    fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * st);
-                    if (valid) rew[st * ep.rs + row] = so.reward;  // per-state planes (SoA): coalesced rows
-                }
-            }
-        } else {
-            const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
-            const bool live = si < nsi;  // states past the caps keep the identity byte
-            const uint64_t to = live ? (uint64_t)(si + so.fill_buy - so.fill_sell) : (uint64_t)si;
-            map = (map & ~(0xFFull << (8 * si))) | (to << (8 * si));
-            traded |= (uint32_t)(live && (so.fill_buy | so.fill_sell)) << si;
-            rl[si * kWave + lane] = so.reward;
-        }
+        const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
+        const bool live = si < nsi;  // states past the caps keep the identity byte
+        const uint64_t to = live ? (uint64_t)(si + so.fill_buy - so.fill_sell) : (uint64_t)si;
+        map = (map & ~(0xFFull << (8 * si))) | (to << (8 * si));
+        traded |= (uint32_t)(live && (so.fill_buy | so.fill_sell)) << si;
+        rl[si * kWave + lane] = so.reward;
     };
-    if constexpr (MODE == 0) {
-        layer12(0, 0);
-#pragma unroll
-        for (int si = 0; si < NSI; ++si) {
-            __builtin_amdgcn_sched_barrier(0);
-            if (si + 1 < NSI) layer12(si + 1, (si + 1) & 1);
-            transpose(si & 1);
-            layer3_env(si);
-        }
-    } else {
-        // one accumulator set; per state a vector block (transpose of state
-        // si, layer 1 of si+1, layer 3 + FPT step of si) and a pure MFMA block
-        // (layer 2 of si+1): f32 MFMAs and vector ops of ONE wave do not
-        // overlap on gfx950 (tools/mb/mb_mfma_valu.hip), so the blocks are
-        // kept apart and the overlap comes from the other waves of the SIMD
+    {
         float h1[KS][4];
         auto layer1 = [&](int si) {
             const float x2 = (float)((double)(inv_min + si) / 2.0);
@@ -807,8 +738,8 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
                 for (int q = 0; q < 4; ++q)
 #pragma unroll
                     for (int rt = 0; rt < NT; ++rt)
-                        acc[0][q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[i][q],
-                                                                             i == 0 ? b2c[rt] : acc[0][q][rt], 0, 0, 0);
+                        acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[i][q],
+                                                                          i == 0 ? b2c[rt] : acc[q][rt], 0, 0, 0);
         };
         layer1(0);
         SGMM_TSTAMP(wslot, 1, h1[KS - 1][3] + pre[0][0] + w2f[0][0] + b2c[0][0]);
@@ -824,7 +755,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
             SGMM_V3T(st_a);
             st_m += st_a - st_b;
 #endif
-            transpose(0);
+            transpose();
             if (si + 1 < NSI) layer1(si + 1);
             layer3_env(si);
             __builtin_amdgcn_sched_barrier(0);
@@ -836,11 +767,7 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    SGMM_TSTAMP(wslot, 2, map + traded + fw);
-    if constexpr (ARL) {
-        if (valid) fills[row] = fw;
-        return;
-    }
+    SGMM_TSTAMP(wslot, 2, map + traded);
     if (!valid) {  // padded lanes: identity steps, no trades
         map = kIdentityMap;
         traded = 0;
@@ -904,11 +831,8 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
-constexpr int kFrontierMaxWaves = 2;   // waves (64-chunk groups) per episode
-constexpr int kFrontierSlots = kFrontierLanes * kFrontierMaxWaves;  // chunks per episode (plane padding)
-constexpr int kFrontierSegs = 4;       // tick segments per chunk of a whole episode (hand-offs + 1)
-constexpr int kFrontierRecs = kFrontierLanes * kFrontierSegs;  // chunk records per episode: e * 256 + k * 64 + c
-static_assert(kFrontierRecs >= kFrontierSlots, "records cover both layouts");
+constexpr int kFrontierMaxWaves = 4;   // waves (64-chunk groups) per episode
+constexpr int kFrontierRecs = kFrontierLanes * kFrontierMaxWaves;  // chunk records per episode: e * 256 + c
 constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
 typedef __attribute__((address_space(3))) const float lds_cf;
 typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
@@ -918,14 +842,12 @@ __host__ __device__ __forceinline__ int frontier_len(int T, int nw) {
     return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
 }
 // the episode's block of plane rows: nw groups of frontier_len(T, nw) x 64 rows
-// <= T + 512 rows (T rounded up to 64 nw chunks of a multiple of 4), starting
-// on a 128-byte line (16 rows), so blocks at step_off + 528 e (rounded up to
-// 16) never overlap and no two episodes share a line -- a scan of the fused
-// launch may read its episode while a neighbour's walk still writes; the plane
-// stride covers total_steps + 528 n (rew_stride).  Group g's row of tick
-// offset u, lane l: base + g * CL * 64 + u * 64 + l (tick-offset-major within
-// the group)
-constexpr int kFrontierPad = 4 * kFrontierSlots + 16;  // plane rows per episode beyond its ticks
+// <= T + 256 nw rows (T rounded up to 64 nw chunks of a multiple of 4),
+// starting on a 128-byte line (16 rows), so blocks at step_off + 1040 e
+// (rounded up to 16) never overlap and no two episodes share a line; the plane
+// stride covers total_steps + 1040 n (rew_stride).  Group g's rows start at
+// base + g * CL * 64 (frontier_row within the group)
+constexpr int kFrontierPad = 4 * kFrontierRecs + 16;  // plane rows per episode beyond its ticks
 __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
     return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
 }
@@ -1377,13 +1299,11 @@ __device__ __forceinline__ void validation_tail(const StepArgs& sa, double v, in
 //   2. every thread: the rewards of its 4 ticks from the path plane of their
 //      chunk's start state (one coalesced row per chunk) -> LDS;
 //   3. the rewards' sequential float64 sum, bit-exact (exact_sum_window).
-// FR: the frontier kernel's chunks (frontier_len(T, nw) ticks, at most 64 per
-// wave, slots e * 128 + c, u32 trade counts, kinfo = merge tick | p0 << 29).
+// FR: the frontier kernel's chunks (frontier_len(T, nw) ticks, 64 per wave,
+// records e * 256 + c, u32 trade counts, kinfo = merge tick | p0 << 29).
 // TPB < NT: a TPB-thread workgroup with NT's window and block layout (TPB =
 // 64, NT = 256: one wave -- the only one exact_sum_window<256> gives blocks
 // to -- gathers 1024 values, so many more episodes run per CU).
-// SC1: the walk's outputs were handed over inside this launch (the fused
-// frontier kernel): every load of them is an sc1 load (ld_rec<true>).
 template <int NT>
 struct ScanShared {
     double* sel;          // [NT * kSumTpt] the window (the last block padded in place)
@@ -1394,10 +1314,7 @@ struct ScanShared {
     unsigned char* tail;  // generation-tail scratch (aliases sel)
 };
 
-// SEG: the episode's chunks may be cut into tick segments (the hand-off
-// launch); without it the gather indexes chunk records directly (the segment
-// lookup cost the config-3 scan ~14 us)
-template <int NSM, int NT, bool FR, int TPB, bool SC1, bool TAIL = true, bool SEG = false>
+template <int NSM, int NT, bool FR, int TPB>
 __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, const sgmm_env_params* __restrict__ params,
                                              int32_t inv_min, const uint64_t* __restrict__ cmaps,
                                              const uint64_t* __restrict__ ctr, const uint32_t* __restrict__ kinfo,
@@ -1415,56 +1332,13 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     const int64_t so = ep.step_off[e];
     const int64_t cb = FR ? (int64_t)e * kFrontierRecs : (int64_t)chunk_base(so, e);
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
-    // segmented chunks (whole frontier episodes whose walks handed ticks over):
-    // the segments in tick order -- ord[j] = record block of the j-th, bnd[j] =
-    // its first chunk offset (INT_MAX past the last); uniform
-    int nseg = 1, ord[kFrontierSegs] = {0, 1, 2, 3}, bnd[kFrontierSegs] = {0, INT_MAX, INT_MAX, INT_MAX};
-    if (FR && SEG && nw == 1 && ep.fseg) {
-        nseg = (int)min((uint32_t)kFrontierSegs, ld_rec<SC1>(ep.fseg + 4 * (int64_t)e));
-        for (int k = 1; k < nseg; ++k) bnd[k] = (int)ld_rec<SC1>(ep.fseg + 4 * (int64_t)e + k);
-        for (int k = 1; k < nseg; ++k)  // insertion sort by offset (segment 0 starts at 0)
-            for (int j = k; j > 1 && bnd[j] < bnd[j - 1]; --j) {
-                const int tb_ = bnd[j], to_ = ord[j];
-                bnd[j] = bnd[j - 1];
-                ord[j] = ord[j - 1];
-                bnd[j - 1] = tb_;
-                ord[j - 1] = to_;
-            }
-    }
     SGMM_STAMP(e, 0);
-    if (FR && SEG && nseg > 1) {  // one round (a whole episode has <= 64 chunks), per chunk its segments in order
-        if (tid < kWave) {
-            const int c = lane;
-            uint64_t mk[kFrontierSegs], M = kIdentityMap;
-#pragma unroll
-            for (int j = 0; j < kFrontierSegs; ++j) {
-                mk[j] = (j < nseg && c < nch) ? ld_rec<SC1>(cmaps + cb + ord[j] * kFrontierLanes + c) : kIdentityMap;
-                M = map_then(M, mk[j]);
-            }
-            const uint64_t inc = wave_map_scan(M);
-            uint64_t excl = shfl_up_u64(inc, 1);
-            if (lane == 0) excl = kIdentityMap;
-            uint32_t st = map_get(excl, (uint32_t)(-inv_min));
-            int tr = 0;
-#pragma unroll
-            for (int j = 0; j < kFrontierSegs; ++j)
-                if (j < nseg && c < nch) {
-                    const int v = ord[j] * kFrontierLanes + c;
-                    start[v] = (uint8_t)st;
-                    tr += (int)ld_rec<SC1>(reinterpret_cast<const uint32_t*>(ctr) + (cb + v) * 8 + st);
-                    kin[v] = ld_rec<SC1>(kinfo + cb + v);
-                    st = map_get(mk[j], st);
-                }
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) tr += __shfl_xor(tr, off, kWave);
-            if (lane == 0) *sh.red = tr;
-        }
-    } else if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
+    if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
         uint32_t s = (uint32_t)(-inv_min);
         int tr = 0;
         for (int c0 = 0; c0 < nch; c0 += kWave) {
             const int c = c0 + lane;
-            const uint64_t m = c < nch ? ld_rec<SC1>(cmaps + cb + c) : kIdentityMap;
+            const uint64_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
             const uint64_t k = (!FR && c < nch) ? ctr[cb + c] : 0;
             const uint64_t inc = wave_map_scan(m);
             uint64_t excl = shfl_up_u64(inc, 1);
@@ -1473,8 +1347,8 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
             if (c < nch) start[c] = (uint8_t)st;
             if (FR) {
                 if (c < nch) {
-                    tr += (int)ld_rec<SC1>(reinterpret_cast<const uint32_t*>(ctr) + (cb + c) * 8 + st);
-                    kin[c] = ld_rec<SC1>(kinfo + cb + c);
+                    tr += (int)reinterpret_cast<const uint32_t*>(ctr)[(cb + c) * 8 + st];
+                    kin[c] = kinfo[cb + c];
                 }
             } else {
                 tr += (int)((k >> (8 * st)) & 0xFFu);
@@ -1508,49 +1382,37 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
             if (i0 < n) {
                 if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
                     const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
-                    // the record of the segment holding offset u (segment offsets are
-                    // multiples of kSumTpt: a thread's ticks lie in one segment)
-                    const int v = SEG ? ord[(u >= bnd[1]) + (u >= bnd[2]) + (u >= bnd[3])] * kFrontierLanes + c : c;
-                    const uint32_t ki = kin[v];
+                    const uint32_t ki = kin[c];
                     const int kc = (int)(ki & 0x1FFFFFFFu);
-                    const int64_t pst = start[v], pp0 = ki >> 29;
+                    const int64_t pst = start[c], pp0 = ki >> 29;
 #ifdef SGMM_PLANE1
                     const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        c % kFrontierLanes;
 #pragma unroll
                     for (int j = 0; j < kSumTpt; ++j) {
                         const int jj = min(j, n - 1 - i0);
-                        r[g][j] = ld_rec<SC1>(rew + (u + jj >= kc ? pp0 : pst) * ep.rs + rb +
-                                              (int64_t)(u + jj) * kFrontierLanes);
+                        r[g][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
                     }
 #else
                     // the chunk's 4 ticks u .. u + 3 are 32 contiguous bytes (frontier_row)
                     const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        frontier_row(u, c % kFrontierLanes);
-                    if constexpr (SC1) {
-#pragma unroll
-                        for (int j = 0; j < kSumTpt; ++j) {
-                            const int jj = min(j, n - 1 - i0);
-                            r[g][j] = ld_rec<true>(rew + (u + jj >= kc ? pp0 : pst) * ep.rs + rb + jj);
-                        }
-                    } else {
-                        // one plane for the 4 ticks unless the paths merge inside them
-                        double2 a0{0.0, 0.0}, a1{0.0, 0.0}, b0{0.0, 0.0}, b1{0.0, 0.0};
-                        if (u < kc) {
-                            const double2* pa = reinterpret_cast<const double2*>(rew + pst * ep.rs + rb);
-                            a0 = pa[0];
-                            a1 = pa[1];
-                        }
-                        if (u + kSumTpt - 1 >= kc) {
-                            const double2* pb = reinterpret_cast<const double2*>(rew + pp0 * ep.rs + rb);
-                            b0 = pb[0];
-                            b1 = pb[1];
-                        }
-                        r[g][0] = u >= kc ? b0.x : a0.x;
-                        r[g][1] = u + 1 >= kc ? b0.y : a0.y;
-                        r[g][2] = u + 2 >= kc ? b1.x : a1.x;
-                        r[g][3] = u + 3 >= kc ? b1.y : a1.y;
+                    // one plane for the 4 ticks unless the paths merge inside them
+                    double2 a0{0.0, 0.0}, a1{0.0, 0.0}, b0{0.0, 0.0}, b1{0.0, 0.0};
+                    if (u < kc) {
+                        const double2* pa = reinterpret_cast<const double2*>(rew + pst * ep.rs + rb);
+                        a0 = pa[0];
+                        a1 = pa[1];
                     }
+                    if (u + kSumTpt - 1 >= kc) {
+                        const double2* pb = reinterpret_cast<const double2*>(rew + pp0 * ep.rs + rb);
+                        b0 = pb[0];
+                        b1 = pb[1];
+                    }
+                    r[g][0] = u >= kc ? b0.x : a0.x;
+                    r[g][1] = u + 1 >= kc ? b0.y : a0.y;
+                    r[g][2] = u + 2 >= kc ? b1.x : a1.x;
+                    r[g][3] = u + 3 >= kc ? b1.y : a1.y;
 #endif
                 } else {
                     const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
@@ -1603,14 +1465,14 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
         if (tr == 0) total -= params[ep.param[e]].idle_penalty;  // drl_engine.py:64-65
         store_record(fitness, trades_out, e, total, tr);
     }
-    if (TAIL && step.st) {
+    if (step.st) {
         if (step.mode == 2) validation_tail(step, total, tr, sh.red, e);
         else generation_tail(step, fitness, trades_out, sh.tail, sh.red, e, n_total);
     }
 }
 
 // one workgroup per episode (the table path, and the frontier path unfused)
-template <int NSM, int NT, bool FR, int TPB = NT, bool SEG = false>
+template <int NSM, int NT, bool FR, int TPB = NT>
 __global__ __launch_bounds__(TPB) void k_path_scan(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min,
     const uint64_t* __restrict__ cmaps, const uint64_t* __restrict__ ctr,
@@ -1618,233 +1480,16 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[FR ? (SEG ? kFrontierRecs : kFrontierSlots) : kMaxLen / kChunk];
-    __shared__ uint32_t kin[FR ? (SEG ? kFrontierRecs : kFrontierSlots) : 1];
+    __shared__ uint8_t start[FR ? kFrontierRecs : kMaxLen / kChunk];
+    __shared__ uint32_t kin[FR ? kFrontierRecs : 1];
     __shared__ int red_trades;
     const int e = blockIdx.x;
     const ScanShared<NT> sh{reinterpret_cast<double*>(lds), &L, start, kin, &red_trades, lds};
-    scan_episode<NSM, NT, FR, TPB, false, true, SEG>(e, FR ? (int)ep.fnw[e] : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew,
-                                          fitness, trades_out, step, (int)gridDim.x, sh);
+    scan_episode<NSM, NT, FR, TPB>(e, FR ? ep.ngrp : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness, trades_out,
+                                   step, (int)gridDim.x, sh);
 }
 
 // ------------------------------------------------------------------ frontier kernel (the walk)
-// The fused launch (FUSED): walks and path scans in one kernel.  Blocks
-// [0, nwalk) walk one episode each; when a walk ends, its wave publishes the
-// episode on its XCD's queue (its stores drained, then one lane's agent-scope
-// atomics) and leaves.  Blocks [nwalk, nwalk + nscan) are scanners: each
-// claims episodes from its own XCD's queue and scans them as they arrive, so
-// the scans run in the walks' tail instead of after it.  A scanner waits (with
-// s_sleep) only once every walk has started -- then every pending entry is
-// sure to come -- and otherwise gives up after a bounded wait and leaves; the
-// cleanup launch after the kernel scans whatever is left, so no dispatch order
-// can deadlock the launch.  Producer and consumer share the XCD's L2, so the
-// walk's outputs are plain stores (write-back, whole lines; write-through
-// stores of the 8-byte plane rows were ~100x slower) and the scan reads them
-// with sc1 loads past its own L1; episodes' output blocks never share a line
-// (frontier_base), and a split episode (two waves, maybe on two XCDs) is never
-// fused.
-struct FrontierQueue {
-    uint32_t* ctl;     // per XCD x: ctl[32 x] head (next entry to claim), u64 at ctl + 32 x + 2:
-                       // tail (next free slot) | done << 32 (set once every walk has pushed);
-                       // ctl[32 kXcds] walks started, ctl[32 kXcds + 32] walks finished,
-                       // ctl[32 kXcds + 64] episodes scanned
-    uint32_t* q;       // per XCD x: q[x * n + i] = episode + 1; 0 = not yet stored
-    double* fitness;
-    int32_t* trades;
-    StepArgs step;
-    int32_t n;         // episodes of the launch
-    int32_t nwalk;     // walk blocks (the scanners follow)
-    int32_t poll;      // s_sleep(127) rounds between two polls of an empty queue
-};
-constexpr int kXcds = 8;
-constexpr int kScanPatience = 2048;  // idle polls a scanner waits for walks still to start
-__device__ __forceinline__ uint32_t xcc_id() {
-    uint32_t x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    return x & (kXcds - 1);
-}
-constexpr int kFusedScanNT = 4 * kWave;                             // one-wave scans: 256-thread window layout
-constexpr int kFusedSel = kFusedScanNT * kSumTpt * (int)sizeof(double);  // 8 KB window
-constexpr int kFusedScanLds = kFusedSel + (int)sizeof(SumLds<kFusedScanNT>) + kFrontierRecs +
-                              4 * kFrontierRecs + 16;
-static_assert(sizeof(SumLds<kFusedScanNT>) % 8 == 0, "scan LDS carve-out alignment");
-
-template <class T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-    typedef __attribute__((address_space(1))) T gT;
-    __hip_atomic_store((gT*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <bool SC1, class T>
-__device__ __forceinline__ void st_out(T* p, T v) {
-    if constexpr (SC1) st_sc1(p, v);
-    else *p = v;
-}
-__device__ __forceinline__ uint32_t atomic_peek(uint32_t* p) {  // coherent read (an agent-scope RMW)
-    return __hip_atomic_fetch_add(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t atomic_peek64(uint64_t* p) {
-    return __hip_atomic_fetch_add(p, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t* queue_state(const FrontierQueue& fq, uint32_t x) {
-    return reinterpret_cast<uint64_t*>(fq.ctl + 32 * x + 2);
-}
-
-typedef __attribute__((address_space(3))) unsigned char lds_u8;
-
-// Tick hand-offs between frontier walks (not in the fused launch).  A wave
-// whose walk has ended waits as a helper (while every walk of the launch has
-// started); a walk that sees a helper waiting, with >= min_rem ticks left in
-// its segment, hands the second half of them to the queue: a new segment of
-// the episode's chunks, walked from its first tick with every start state
-// tracked (its start state is known only to the scan), written to its own
-// records.  The walk's paths from a segment start are the same paths, so the
-// outputs stay bit-identical; the tail of the launch (the heaviest walks alone
-// on their SIMDs) is shared out instead.  ctl words, one 128-byte line each:
-// [0] queue head, [32] queue tail, [64] items (walks + segments) not yet
-// finished, [96] helpers waiting, [128] walks started; then the episodes'
-// segment tables (EpArrays::fseg, u32[4 n]), then the queue: q[i] = item i
-// (0 = not yet stored): (e + 1) | segment << 28 | start << 32 | end << 48.
-constexpr int kStHead = 0, kStTail = 32, kStActive = 64, kStIdle = 96, kStStarted = 128;
-constexpr int kStNoSlot = 129, kStQuitEarly = 130;  // diagnostics: refused hand-offs, helpers that left early
-constexpr int kStHelpers = 131;  // waves that became helpers (at most FrontierSteal::max_helpers)
-constexpr int kStCtlWords = 160;
-constexpr int kStealMinRem = 16;  // ticks left in a segment for a hand-off (two halves of >= 8)
-struct FrontierSteal {
-    uint32_t* ctl;  // ctl[kStCtlWords] | fseg[4 n] | u64 q[3 n + 64]
-    int32_t on;
-    int32_t nwalk;
-    int32_t n;      // episodes of the launch
-    int32_t maxseg; // segments per episode allowed (<= kFrontierSegs)
-    int32_t helper_every;  // the finished waves of blocks b % helper_every == 0 stay as helpers
-    int32_t nchk;          // hand-off checks per segment (from half-way, every eighth)
-    __device__ uint32_t* seg(int e) const { return ctl + kStCtlWords + 4 * (int64_t)e; }
-    __device__ uint64_t* q() const { return reinterpret_cast<uint64_t*>(ctl + kStCtlWords + 4 * (int64_t)n); }
-};
-__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
-    typedef __attribute__((address_space(1))) const uint32_t gU;
-    return __hip_atomic_load((gU*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t atomic_add_u32(uint32_t* p, uint32_t v) {
-    return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// The scans of the fused launch, a separate (not inlined) function: its
-// registers are allocated apart from the walk's, so the walk keeps its three
-// waves per SIMD.  `lds` is the wave's LDS block (the walk's, dead by now).
-// A scanner (or, CLEANUP, a block of the cleanup launch, which sweeps every
-// XCD's queue after the fused kernel has ended).
-template <int NSI, bool CLEANUP>
-__device__ __forceinline__ void fused_scans(const EpArrays ep, const sgmm_env_params* __restrict__ params,
-                                            int32_t inv_min, const uint64_t* __restrict__ cmaps,
-                                            const uint32_t* __restrict__ ctr32, const uint32_t* __restrict__ kinfo,
-                                            const double* __restrict__ rew, const FrontierQueue fq, lds_u8* lds) {
-    using SL = SumLds<kFusedScanNT>;
-    typedef __attribute__((address_space(3))) double lds_f64;
-    typedef __attribute__((address_space(3))) SL lds_sl;
-    typedef __attribute__((address_space(3))) uint32_t lds_u32;
-    typedef __attribute__((address_space(3))) int lds_i32;
-    const ScanShared<kFusedScanNT> sh{(double*)(lds_f64*)lds, (SL*)(lds_sl*)(lds + kFusedSel),
-                                      (uint8_t*)(lds + kFusedSel + sizeof(SL)),
-                                      (uint32_t*)(lds_u32*)(lds + kFusedSel + sizeof(SL) + kFrontierRecs),
-                                      (int*)(lds_i32*)(lds + kFusedSel + sizeof(SL) + 5 * kFrontierRecs),
-                                      (unsigned char*)lds};
-    const int lane = threadIdx.x;
-    uint32_t* started = fq.ctl + 32 * kXcds;
-    uint32_t x = CLEANUP ? 0u : xcc_id();
-    int patience = 0;
-#ifdef SGMM_STAMPS
-    // scanner timeline (row 32768 + scanner): start, first claim, end (realtime),
-    // scans, idle polls, XCC, time spent in scans (realtime ticks)
-    unsigned long long sc_t0, sc_first = 0, sc_n = 0, sc_polls = 0, sc_busy = 0;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_t0)::"memory");
-    const int sc_row = 32768 + (CLEANUP ? 16384 + (int)blockIdx.x : (int)blockIdx.x - fq.nwalk);
-#endif
-    while (true) {
-        // 0..: an entry of queue x claimed; -1: queue x empty and no more will
-        // come (or this scanner gives up); -2: empty for now.  An idle poll is
-        // ONE atomic on the XCD's state word (pollers of one word saturate it)
-        int32_t h = -1;
-        if (lane == 0) {
-            uint32_t* head = fq.ctl + 32 * x;
-            const uint64_t sw = CLEANUP ? (1ull << 32) | atomic_peek(reinterpret_cast<uint32_t*>(queue_state(fq, x)))
-                                        : atomic_peek64(queue_state(fq, x));
-            const uint32_t tail = (uint32_t)sw;
-            const bool done = (sw >> 32) != 0;
-            h = done ? -1 : -2;
-            uint32_t cur = atomic_peek(head);
-            while (cur < tail) {  // claim entry cur
-                if (__hip_atomic_compare_exchange_strong(head, &cur, cur + 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)) {
-                    h = (int32_t)cur;
-                    break;
-                }
-            }
-            if (!CLEANUP && h == -2 && (++patience & 63) == 0 && atomic_peek(started) < (uint32_t)fq.nwalk &&
-                patience > kScanPatience)
-                h = -1;  // walks still to start: leave the slot to them (the cleanup launch finishes up)
-        }
-        h = __builtin_amdgcn_readfirstlane(h);
-        if (h == -1) {
-            if (!CLEANUP || ++x == (uint32_t)kXcds) break;
-            continue;
-        }
-        if (h == -2) {
-#ifdef SGMM_STAMPS
-            ++sc_polls;
-#endif
-            for (int i = 0; i < fq.poll; ++i) __builtin_amdgcn_s_sleep(127);
-            continue;
-        }
-        uint32_t ent = 0;
-        if (lane == 0) {  // its pusher has taken the slot and is about to store it
-            uint32_t* q = fq.q + (int64_t)x * fq.n;
-            while ((ent = atomic_peek(&q[h])) == 0u) __builtin_amdgcn_s_sleep(1);
-        }
-        ent = (uint32_t)__builtin_amdgcn_readfirstlane((int)ent);
-#ifdef SGMM_STAMPS
-        unsigned long long sc_a;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_a)::"memory");
-        if (!sc_first) sc_first = sc_a;
-        ++sc_n;
-#endif
-        scan_episode<NSI, kFusedScanNT, true, kWave, true, false>(
-            (int)ent - 1, 1, ep, params, inv_min, cmaps, reinterpret_cast<const uint64_t*>(ctr32), kinfo, rew,
-            fq.fitness, fq.trades, fq.step, fq.n, sh);
-        if (lane == 0) {  // its record stored (sc1) and drained: one more episode scanned
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(fq.ctl + 32 * (kXcds + 2), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#ifdef SGMM_STAMPS
-        {
-            unsigned long long sc_b;
-            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_b)::"memory");
-            sc_busy += sc_b - sc_a;
-        }
-#endif
-        __syncthreads();  // the LDS carve-out is reused by the next scan
-    }
-#ifdef SGMM_STAMPS
-    {
-        unsigned long long sc_t1;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(sc_t1)::"memory");
-        if (lane == 0 && sc_row < kStampWaves) {
-            g_tstamps[sc_row][0] = sc_t0;
-            g_tstamps[sc_row][1] = sc_first;
-            g_tstamps[sc_row][2] = sc_t1;
-            g_tstamps[sc_row][3] = sc_n;
-            g_tstamps[sc_row][4] = sc_polls;
-            g_tstamps[sc_row][5] = x;
-            g_tstamps[sc_row][6] = sc_busy;
-        }
-    }
-#endif
-}
-
-// The frontier kernel's arguments, one struct: a wave walks several items
-// (its walk, then handed-over segments), and each walk reads them afresh
-// through a laundered kernarg pointer -- otherwise the compiler keeps every
-// argument the walk's prologue uses live through the tick loop for the next
-// item (80 SGPRs spilled)
 struct FrontierArgs {
     sgmm_ticks tk;
     EpArrays ep;
@@ -1855,15 +1500,13 @@ struct FrontierArgs {
     uint32_t* ctr32;
     uint32_t* kinfo;
     double* rew;
-    FrontierQueue fq;
-    FrontierSteal fs;
 };
-typedef __attribute__((address_space(4))) const FrontierArgs kFrontierArgsK;
 
-// STEAL: the hand-off variant (a wave walks items in a loop; its prologue
-// spills a few registers outside the tick loop) -- the default launch is the
-// single-walk instantiation, with no loop and no spills
-template <int H, int NSI, bool FUSED, bool STEAL = false>
+// Wave b walks chunk group cg = b % ngrp of the episode at order position
+// b / ngrp (longest episodes first).  (Round 3's walks with tick hand-offs and
+// the launch with the path scans fused in measured no faster:
+// tools/experiments/round3_opt_in_paths.patch.)
+template <int H, int NSI>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
@@ -1871,72 +1514,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
     // LDS (~13 KB per wave, so 3 waves per SIMD fit): the genome is staged in
     // `big`, the weights the loop needs are copied out, then `big` holds the
-    // half-activation transpose buffer and the per-state rewards; a scanner
-    // (FUSED) holds its window, records and chunk tables there
-    constexpr int kWalkBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
-    constexpr int kBig = (FUSED && kFusedScanLds > kWalkBig) ? kFusedScanLds : kWalkBig;
+    // half-activation transpose buffer and the per-state rewards
+    constexpr int kBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
     __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
-    const FrontierQueue& fq = args.fq;
-    const FrontierSteal& fs = args.fs;
-    if constexpr (FUSED) {
-        if ((int)blockIdx.x >= fq.nwalk) {  // a scanner
-            fused_scans<NSI, false>(args.ep, args.params, args.inv_min, args.cmaps, args.ctr32, args.kinfo, args.rew,
-                                    fq, (lds_u8*)big);
-            return;
-        }
-        if (threadIdx.x == 0)
-            __hip_atomic_fetch_add(fq.ctl + 32 * kXcds, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // wave b: the whole episode at order position b (b < fwhole), else chunk
-    // group g of a split episode (two waves each, longest episodes first)
-    const int b = (int)blockIdx.x;
-    const int fwhole = args.ep.fwhole;
-    const int pos = b < fwhole ? b : fwhole + ((b - fwhole) >> 1);
-    const int nw0 = b < fwhole ? 1 : 2, cg0 = b < fwhole ? 0 : (b - fwhole) & 1;
-    const int e0 = args.ep.order ? args.ep.order[pos] : pos;
-    if (cg0 == 0 && threadIdx.x == 0) {
-        if (!FUSED) args.ep.fnw[e0] = (uint32_t)nw0;  // fused: the queue entry carries it
-        // one tick segment so far (before any hand-off's add to the same word)
-        if (!FUSED && fs.on)
-            __hip_atomic_exchange(fs.seg(e0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // the last workgroup of the grid has started (so, dispatched in order, have
-    // all the walks): ctl[kStStarted]; ctl[kStActive] starts at the walk count
-    if (!FUSED && fs.on && threadIdx.x == 0 && b == (int)gridDim.x - 1) st_sc1(fs.ctl + kStStarted, 1u);
-
     // (13 200 bytes of LDS per wave for H = 32 with `big`: twelve waves fit a
-    // CU's 160 KiB in 512-byte granules, the walks and the scanners of a
-    // 3-waves-per-SIMD grid; 13 328 bytes allowed only eleven)
+    // CU's 160 KiB in 512-byte granules; 13 328 bytes allowed only eleven)
     __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
     __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
     __shared__ __attribute__((aligned(16))) float b2s[H];
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
     // successor (bits 9-11) and the fill (bit 12) written back by the column
     __shared__ uint16_t pl[kWave * (NSI - 1)];
-    __shared__ uint32_t st_ctx[5];  // hand-offs: episode, control pointer, episode count
 
-    // walk chunk group cg of episode e over chunk offsets [ub, ue) (ue < 0: the
-    // chunk length) as tick segment kseg; can_split: may hand ticks over
-    auto walk = [&](const FrontierArgs& A, const int e, const int nw, const int cg, const int kseg, const int ub,
-                    int ue, const bool can_split) {  // (returns early past its last chunk)
-    const sgmm_ticks& tk = A.tk;
-    const EpArrays& ep = A.ep;
-    const sgmm_env_params* __restrict__ params = A.params;
-    const GenomeSrc& src = A.src;
-    const int32_t inv_min = A.inv_min, nsi = A.nsi;
-    uint64_t* __restrict__ cmaps = A.cmaps;
-    uint32_t* __restrict__ ctr32 = A.ctr32;
-    uint32_t* __restrict__ kinfo = A.kinfo;
-    double* __restrict__ rew = A.rew;
+    const sgmm_ticks& tk = args.tk;
+    const EpArrays& ep = args.ep;
+    const sgmm_env_params* __restrict__ params = args.params;
+    const GenomeSrc& src = args.src;
+    const int32_t inv_min = args.inv_min, nsi = args.nsi;
+    uint64_t* __restrict__ cmaps = args.cmaps;
+    uint32_t* __restrict__ ctr32 = args.ctr32;
+    uint32_t* __restrict__ kinfo = args.kinfo;
+    double* __restrict__ rew = args.rew;
+    const int nw = ep.ngrp;
+    const int pos = (int)blockIdx.x / nw, cg = (int)blockIdx.x - pos * nw;
+    const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
     const int CL = frontier_len(T, nw);
-    if (ue < 0) ue = CL;
     const int nch = (T + CL - 1) / CL;
     if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
-    int lane_ = (int)threadIdx.x;
-    if constexpr (STEAL) asm volatile("" : "+v"(lane_));  // per item: lane-derived addresses not kept live across items
-    const int lane = lane_, grp = lane >> 4, col = lane & 15;
+    const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
     const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
@@ -1968,7 +1575,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     // per-lane path bookkeeping: byte s of cur = the state of the path that
     // started the chunk in state s (tracked starts: bits of sset)
     const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = c >= nch ? 0u : ((c == 0 && ub == 0) ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
     const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
     uint64_t cur = kIdentityMap;
     // trade count along the path from each tracked start: 16 bits per start,
@@ -1977,7 +1584,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
     for (int s = 0; s < (NSI + 1) / 2; ++s) cnt[s] = 0;
     bool merged = __builtin_popcount(sset) <= 1;
-    int kc = merged ? ub : CL;  // merge offset (CL: not within the segment)
+    int kc = merged ? 0 : CL;  // merge offset (CL: never)
     auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
 #ifdef SGMM_STAMPS
     // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
@@ -1994,60 +1601,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
     SGMM_FT(fs_t0);
 #endif
-    int64_t ti = tick_of(ub);
+    int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
-    // hand-off checks at 1/2, 5/8 and 3/4 of the segment: each reads one global
-    // word (every walk polling it every few ticks made it a hot spot that cost
-    // the walks a third of their speed); the tail's walks are past half-way
-    // when the first helpers appear
-    const int chk_step = max(4, ((ue - ub) >> 3) & ~3);
-    const int chk_max = (int)A.fs.nchk;  // checks per segment
-    int next_chk = (STEAL && can_split) ? ub + (((ue - ub) >> 1) & ~3) : INT_MAX, nchk = 0;
-    // what a hand-off needs, parked in LDS (not held in registers through the loop)
-    if (STEAL && threadIdx.x == 0) {
-        st_ctx[0] = (uint32_t)e;
-        st_ctx[1] = (uint32_t)reinterpret_cast<uint64_t>(A.fs.ctl);
-        st_ctx[2] = (uint32_t)(reinterpret_cast<uint64_t>(A.fs.ctl) >> 32);
-        st_ctx[3] = (uint32_t)A.fs.n | ((uint32_t)A.fs.maxseg << 28);
-        st_ctx[4] = (uint32_t)A.fs.nchk;
-    }
 #pragma unroll 1
-    for (int tt = ub; tt < ue; ++tt) {
-        if (STEAL && tt == next_chk) {
-            next_chk = ++nchk < chk_max ? next_chk + chk_step : INT_MAX;
-            // a helper waits and >= kStealMinRem ticks are left: the second
-            // half of them (from a multiple of 4, so a scan thread's ticks stay
-            // in one segment) becomes a new segment on the queue
-            const uint32_t idle = (uint32_t)__builtin_amdgcn_readfirstlane(
-                (int)ld_sc1_u32(reinterpret_cast<uint32_t*>((uint64_t)st_ctx[1] | ((uint64_t)st_ctx[2] << 32)) + kStIdle));
-            if ((int)idle > 0 && ue - tt >= kStealMinRem) {
-                const int m = tt + (((ue - tt) >> 1) & ~3);
-                int ok = 0;
-                if (threadIdx.x == 0) {
-                    const uint32_t ce = st_ctx[0];
-                    FrontierSteal f{reinterpret_cast<uint32_t*>((uint64_t)st_ctx[1] | ((uint64_t)st_ctx[2] << 32)), 1, 0,
-                                    (int32_t)(st_ctx[3] & 0x0FFFFFFFu), (int32_t)(st_ctx[3] >> 28), 0, 0};
-                    uint32_t* sg = f.seg((int)ce);
-                    // reserve a waiting helper (the read above may be stale)
-                    const int avail = (int)atomic_add_u32(f.ctl + kStIdle, 0xFFFFFFFFu);
-                    const uint32_t kk = avail >= 1 ? atomic_add_u32(sg, 1u) : 0xFFFFu;
-                    if (avail >= 1 && kk < (uint32_t)f.maxseg) {
-                        st_sc1(sg + kk, (uint32_t)m);
-                        atomic_add_u32(f.ctl + kStActive, 1u);
-                        const uint32_t slot = atomic_add_u32(f.ctl + kStTail, 1u);
-                        __hip_atomic_exchange(f.q() + slot,
-                                              (uint64_t)(ce + 1) | ((uint64_t)kk << 28) | ((uint64_t)m << 32) |
-                                                  ((uint64_t)ue << 48),
-                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok = 1;
-                    } else {
-                        atomic_add_u32(f.ctl + kStIdle, 1u);  // give the reservation back
-                        if (avail >= 1) atomic_add_u32(f.ctl + kStNoSlot, 1u);
-                    }
-                }
-                if (__builtin_amdgcn_readfirstlane(ok)) ue = m;
-            }
-        }
+    for (int tt = 0; tt < CL; ++tt) {
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_a);
 #endif
@@ -2418,164 +1975,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = (int64_t)e * kFrontierRecs + kseg * kFrontierLanes + c;
+        const int64_t ci = (int64_t)e * kFrontierRecs + c;
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
         kinfo[ci] = (uint32_t)kc | (p0 << 29);
-    }
-    };
-    // the launch's own walk, then (hand-offs on) the segments handed over to this wave
-    int w_e = e0, w_nw = nw0, w_cg = cg0, w_k = 0, w_ub = 0, w_ue = -1;
-    int registered = 0;  // lane 0: counted among the waiting helpers
-    int helper = 0;      // this wave's own walk is done
-#ifdef SGMM_STAMPS
-    // hand-off timeline (rows 49152 + b): start, own walk's end, exit, items walked, XCC
-    unsigned long long hs_t0, hs_t1 = 0, hs_n = 0;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(hs_t0)::"memory");
-#endif
-#pragma unroll 1
-    while (true) {
-        const kFrontierArgsK* ka = (const kFrontierArgsK*)__builtin_amdgcn_kernarg_segment_ptr();
-        asm volatile("" : "+s"(ka));  // re-read per item (see FrontierArgs)
-        walk(*(const FrontierArgs*)ka, w_e, w_nw, w_cg, w_k, w_ub, w_ue,
-             STEAL && !FUSED && fs.on && w_nw == 1);
-        if constexpr (FUSED) {
-            const int e = e0;
-            const int lane = threadIdx.x;
-            // publish on this XCD's queue: the wave's stores drained into the L2,
-            // then one lane's atomics (every episode is one wave here); the push
-            // completes before the walk counts as finished
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (lane == 0) {
-                const uint32_t x = xcc_id();
-                const uint32_t slot = (uint32_t)__hip_atomic_fetch_add(queue_state(fq, x), (uint64_t)1, __ATOMIC_RELAXED,
-                                                                       __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_exchange(&fq.q[(int64_t)x * fq.n + slot], (uint32_t)(e + 1), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const uint32_t fin = __hip_atomic_fetch_add(fq.ctl + 32 * kXcds + 32, 1u, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                if (fin + 1 == (uint32_t)fq.nwalk)  // the last walk: every push is done, tell the scanners
-                    for (uint32_t y = 0; y < (uint32_t)kXcds; ++y)
-                        __hip_atomic_fetch_add(queue_state(fq, y), 1ull << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            break;
-        }
-        if (!STEAL || !fs.on) break;
-        // helper: walk handed-over segments until none is queued and no walk or
-        // segment is still running (every wave reaches that exit: items only
-        // come from running ones, and a walk's own hand-offs are on the queue
-        // before it finishes)
-        const int lane = threadIdx.x;
-        int got = -1, quit = 0;
-#ifdef SGMM_STAMPS
-        ++hs_n;
-        if (!helper) asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(hs_t1)::"memory");
-#endif
-        if (lane == 0) {
-            atomic_add_u32(fs.ctl + kStActive, 0xFFFFFFFFu);  // this item is done
-            if (!helper) {  // this wave's own walk: stay as a helper?
-                if (b % fs.helper_every != 0) {
-                    quit = 1;  // one wave in helper_every stays
-                } else if (ld_sc1_u32(fs.ctl + kStStarted) == 0u) {
-                    quit = 1;  // walks may still wait for a wave slot: leave this one to them
-                    atomic_add_u32(fs.ctl + kStQuitEarly, 1u);
-                }
-            }
-        }
-        helper = 1;
-        quit = __builtin_amdgcn_readfirstlane(quit);
-#pragma unroll 1
-        while (!quit) {
-            if (lane == 0) {
-                // a few hundred helpers at most, each polling every ~7 us with
-                // read-modify-writes (loads could return stale L2 copies)
-                uint32_t h = atomic_peek(fs.ctl + kStHead);
-                const uint32_t t = atomic_peek(fs.ctl + kStTail);
-                while (h < t) {
-                    if (__hip_atomic_compare_exchange_strong(fs.ctl + kStHead, &h, h + 1, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        got = (int)h;
-                        break;
-                    }
-                }
-                if (got >= 0) {
-                    registered = 0;  // its reservation was taken by the donor (or is taken later)
-                } else if (atomic_peek(fs.ctl + kStActive) == 0u &&
-                           atomic_peek(fs.ctl + kStHead) >= atomic_peek(fs.ctl + kStTail)) {
-                    quit = 1;
-                } else if (!registered) {
-                    atomic_add_u32(fs.ctl + kStIdle, 1u);
-                    registered = 1;
-                }
-            }
-            got = __builtin_amdgcn_readfirstlane(got);
-            if (got >= 0 || __builtin_amdgcn_readfirstlane(quit)) break;
-            __builtin_amdgcn_s_sleep(127);
-            __builtin_amdgcn_s_sleep(127);
-        }
-        if (got < 0) break;
-        uint64_t it = 0;
-        if (lane == 0) {  // its donor has taken the slot and is about to store it
-            while ((it = atomic_peek64(fs.q() + got)) == 0ull) __builtin_amdgcn_s_sleep(1);
-            __hip_atomic_store(fs.q() + got, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // clean slot
-        }
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)it);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(it >> 32));
-        w_e = (int)(lo & 0x0FFFFFFFu) - 1;
-        w_k = (int)(lo >> 28);
-        w_ub = (int)(hi & 0xFFFFu);
-        w_ue = (int)(hi >> 16);
-        w_nw = 1;
-        w_cg = 0;
-        __syncthreads();  // the previous walk's LDS is reused
-    }
-#ifdef SGMM_STAMPS
-    if (!FUSED && fs.on && threadIdx.x == 0 && 49152 + b < kStampWaves) {
-        unsigned long long t2;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t2)::"memory");
-        g_tstamps[49152 + b][0] = hs_t0;
-        g_tstamps[49152 + b][1] = hs_t1;
-        g_tstamps[49152 + b][2] = t2;
-        g_tstamps[49152 + b][3] = hs_n;
-        g_tstamps[49152 + b][4] = xcc_id();
-    }
-#endif
-}
-
-// After the fused launch: scans any episode its scanners left (normally
-// none), then -- every episode scanned -- runs each population's GA tail
-// (the tell, or the validation bookkeeping of mode 2): block k takes
-// population k.  The scanners carry no tail code: it would not fit their
-// registers beside the walk's.
-template <int NSI>
-__global__ __launch_bounds__(kWave) void k_frontier_cleanup(EpArrays ep, const sgmm_env_params* __restrict__ params,
-                                                             int32_t inv_min, const uint64_t* __restrict__ cmaps,
-                                                             const uint32_t* __restrict__ ctr32,
-                                                             const uint32_t* __restrict__ kinfo,
-                                                             const double* __restrict__ rew, FrontierQueue fq) {
-    __shared__ __attribute__((aligned(16))) unsigned char big[kFusedScanLds];
-    fused_scans<NSI, true>(ep, params, inv_min, cmaps, ctr32, kinfo, rew, fq, (lds_u8*)big);
-    const StepArgs& sa = fq.step;
-    if (!sa.st) return;
-    const int n_eps = sa.pop_eps > 0 ? sa.pop_eps : fq.n;
-    const int K = fq.n / n_eps;
-    if ((int)blockIdx.x >= K) return;
-    if (threadIdx.x == 0) {  // the leftovers are scanned by blocks of this launch, all resident
-        while (atomic_peek(fq.ctl + 32 * (kXcds + 2)) < (uint32_t)fq.n) __builtin_amdgcn_s_sleep(8);
-    }
-    __syncthreads();
-    __shared__ int flag;
-    for (int k = blockIdx.x; k < K; k += gridDim.x) {
-        if (sa.mode == 2) {  // one validation episode per population: episode k
-            const double v = ld_rec<true>(fq.fitness + k);
-            const int32_t vtr = ld_rec<true>(fq.trades + k);
-            validation_tail(sa, v, vtr, &flag, k);
-        } else {
-            tail_run(sa, fq.fitness, fq.trades, big, k, n_eps);
-        }
-        __syncthreads();
     }
 }
 
@@ -2918,21 +2322,18 @@ static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + kFrontierP
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps, e->n), e->order, e->n, nullptr, nullptr};
+                    e->param, rew_stride(e->total_steps, e->n), e->order, 1};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Table kernel selection: 0 = f32 MFMA (default for H >= 16), 1 = VALU
-// (one lane per (tick, state)).  SGMM_TABLE_PATH=valu forces the VALU kernel
-// (A/B measurements and as an independent cross-check in the tests).
-static int table_path() {
+// Policy kernel selection, SGMM_TABLE_PATH: unset = the default (frontier
+// kernel for many episodes, else the f32-MFMA table); "frontier" / "table"
+// force either; "valu" forces the VALU table (one lane per (tick, state)), an
+// independent cross-check in the tests.
+static bool table_valu() {
     const char* e = std::getenv("SGMM_TABLE_PATH");
-    if (e && std::strcmp(e, "valu") == 0) return 1;
-    if (e && std::strcmp(e, "v2") == 0) return 2;  // k_policy_table_mfma without the v3 schedule
-    if (e && std::strcmp(e, "v3i") == 0) return 3;  // v3 with two accumulator sets, blocks interleaved
-    if (e && std::strcmp(e, "v3") == 0) return 4;   // v3 (the default without the adversary; opt-in with it)
-    return 0;
+    return e && std::strcmp(e, "valu") == 0;
 }
 
 }  // namespace sgmm
@@ -2970,15 +2371,8 @@ static size_t ws_cmaps(int32_t n, int64_t steps) {
 static size_t ws_ctr(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps) * sizeof(uint64_t), n_frontier_slots(n) * 8 * sizeof(uint32_t)));
 }
-// u32 kinfo[n * 256] | u32 waves[n] | (256-aligned) the fused launch's queues:
-// u32 ctl[11][32] (head, tail per XCD; walks started; walks finished;
-// episodes scanned), u32 q[8][n] | (256-aligned) the hand-offs: control words
-// u32[160], segment tables u32[4 n], queue u64[3 n + 64] -- both zeroed by the
-// launch that uses them
-static size_t ws_kinfo_head(int32_t n) { return align256((n_frontier_slots(n) + (size_t)n) * sizeof(uint32_t)); }
-static size_t ws_queue(int32_t n) { return 4 * 32 * (kXcds + 3) + (size_t)4 * kXcds * n; }
-static size_t ws_steal(int32_t n) { return 4 * (size_t)kStCtlWords + 16 * (size_t)n + 8 * (3 * (size_t)n + 64); }
-static size_t ws_kinfo(int32_t n) { return ws_kinfo_head(n) + align256(ws_queue(n)) + align256(ws_steal(n)); }
+// u32 kinfo[n * 256]: per chunk record the merge tick | p0 << 29
+static size_t ws_kinfo(int32_t n) { return align256(n_frontier_slots(n) * sizeof(uint32_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 
 // The workspace of a batch with n_inventory inventory values, with or
@@ -3029,17 +2423,12 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     return eps->n >= min_eps;
 }
 
-// How many episodes run as one wave in the frontier kernel (the longest
-// fwhole of the order); the rest are split into two waves (two 64-chunk
-// groups of half the length, at the cost of more start-state paths to
-// merge).  Default: every episode whole.  SGMM_FRONTIER_NW=2 splits all,
-// SGMM_FRONTIER_NW=3 balances to 3 x SIMDs waves (every SIMD holds three
-// waves: 2560 episodes on 1024 SIMDs -> 2048 whole + 512 split = 3072 waves).
-// The balance won before the packed extra slots (config 3: 727-736 vs 753 us
-// policy kernel); with packing, all-whole gives the faster generation over a
-// 100-generation run (659 vs 670 us, tools/gpu_nw2.sh): a split episode's
-// second group tracks all five start states until they merge, and packing
-// does not remove that work.
+// Chunk groups per episode in the frontier kernel (one wave each).  A walk's
+// time is set by its serial chain of ticks, not by its SIMD's load, so when the
+// launch has fewer walks than the chip has wave slots (3 per SIMD) the
+// episodes are cut into 2-4 groups of 64 chunks of proportionally fewer ticks;
+// each extra group pays for tracking every start state of its chunks until
+// their paths merge.  SGMM_FRONTIER_NW=1..4 forces the count.
 static int simd_count() {
     static int n = 0;
     if (n == 0) {
@@ -3051,31 +2440,14 @@ static int simd_count() {
     }
     return n;
 }
-// SGMM_FRONTIER_FUSED=1: the frontier kernel scans finished episodes itself
-// (FrontierQueue scanners + the cleanup launch) instead of the separate
-// one-wave path-scan launch.  Off by default: measured slower on config 3
-// (783 vs 734 us per generation) -- scans beside the
-// walks' tail slow those walks, and the last walks' scans still follow them.
-static bool frontier_fused() {
-    const char* v = std::getenv("SGMM_FRONTIER_FUSED");
-    return v && std::strcmp(v, "1") == 0;
-}
-// SGMM_FRONTIER_STEAL=1: tick hand-offs between frontier walks (FrontierSteal).
-// Opt-in: bit-exact (tests/test_gpu_frontier.py) but no faster on config 3
-// (DESIGN.md section 5.1): the walks of the tail are past their hand-off
-// checks when the first helpers appear, and more helpers or checks make their
-// polling of the shared words cost more than the hand-offs save.
-static bool frontier_steal() {
-    const char* v = std::getenv("SGMM_FRONTIER_STEAL");
-    return v && std::strcmp(v, "1") == 0;
-}
-static int32_t frontier_whole(int32_t n) {
-    const char* v = std::getenv("SGMM_FRONTIER_NW");
-    const int mode = v ? std::atoi(v) : 1;
-    if (mode == 2) return 0;
-    if (mode != 3) return n;
-    const int64_t split = std::min<int64_t>(n, std::max<int64_t>(0, 3LL * simd_count() - n));
-    return (int32_t)(n - split);
+static int32_t frontier_groups(int32_t n) {
+    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
+        const int g = std::atoi(v);
+        if (g >= 1 && g <= kFrontierMaxWaves) return g;
+    }
+    if (n <= 0) return 1;
+    const int64_t slots = 3LL * simd_count();
+    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierMaxWaves, slots / n));
 }
 
 template <int H>
@@ -3086,31 +2458,13 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
     if constexpr (H <= 32) {
-        const int tp = table_path();
-        // the adversary on the v3 schedule: opt-in (SGMM_TABLE_PATH=v3) -- measured
-        // slower than k_policy_table_mfma's there (config 4: 159.5 vs 153-155 us; the
-        // 4 FPT steps per state weigh on the vector block the MFMA stream waits for)
-        if (arl && tp == 4) {
+        if (!arl) {
             if (nsi <= 5)
-                SGMM_LAUNCH((k_policy_table_v3<H, 5, 1, true>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi,
-                            ctr, cmaps, fills, rew);
+                SGMM_LAUNCH((k_policy_table_v3<H, 5>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
+                            rew);
             else
-                SGMM_LAUNCH((k_policy_table_v3<H, 8, 1, true>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi,
-                            ctr, cmaps, fills, rew);
-            return;
-        }
-        if (!arl && (tp == 0 || tp == 3 || tp == 4)) {
-#define SGMM_TABLE_V3(NSI_, MODE_)                                                                       \
-    SGMM_LAUNCH((k_policy_table_v3<H, NSI_, MODE_, false>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, \
-                ctr, cmaps, fills, rew)
-            if (tp == 3) {
-                if (nsi <= 5) SGMM_TABLE_V3(5, 0);
-                else SGMM_TABLE_V3(8, 0);
-            } else {
-                if (nsi <= 5) SGMM_TABLE_V3(5, 1);
-                else SGMM_TABLE_V3(8, 1);
-            }
-#undef SGMM_TABLE_V3
+                SGMM_LAUNCH((k_policy_table_v3<H, 8>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
+                            rew);
             return;
         }
     }
@@ -3167,37 +2521,23 @@ static int scan_threads(int64_t n) {
     return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : kWave);
 }
 
-template <int NSM, bool FR, bool SEG = false>
-static void launch_path_scan_t(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
-                             const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
-                             const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
-                             int32_t* trades, const StepArgs& step) {
-    if (nt == kWave)
-        SGMM_LAUNCH((k_path_scan<NSM, 4 * kWave, FR, kWave, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
-                    cmaps, ctr, kinfo, rew, fitness, trades, step);
-    else if (nt == kScanThreads)
-        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR, kScanThreads, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
-                    cmaps, ctr, kinfo, rew, fitness, trades, step);
-    else if (nt == 512)
-        SGMM_LAUNCH((k_path_scan<NSM, 512, FR, 512, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    kinfo, rew, fitness, trades, step);
-    else
-        SGMM_LAUNCH((k_path_scan<NSM, 256, FR, 256, SEG>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr,
-                    kinfo, rew, fitness, trades, step);
-}
-
-// the frontier scan with segmented chunks only for the hand-off launch (ep.fseg set)
 template <int NSM, bool FR>
 static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const EpArrays& ep,
                              const sgmm_env_params* params, int32_t inv_min, const uint64_t* cmaps,
                              const uint64_t* ctr, const uint32_t* kinfo, const double* rew, double* fitness,
                              int32_t* trades, const StepArgs& step) {
-    if (FR && ep.fseg)
-        launch_path_scan_t<NSM, true, true>(nt, n, lds, s, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness,
-                                            trades, step);
+    if (nt == kWave)
+        SGMM_LAUNCH((k_path_scan<NSM, 4 * kWave, FR, kWave>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps,
+                    ctr, kinfo, rew, fitness, trades, step);
+    else if (nt == kScanThreads)
+        SGMM_LAUNCH((k_path_scan<NSM, kScanThreads, FR, kScanThreads>), dim3(n), dim3(nt), lds, s, ep, params, inv_min,
+                    cmaps, ctr, kinfo, rew, fitness, trades, step);
+    else if (nt == 512)
+        SGMM_LAUNCH((k_path_scan<NSM, 512, FR, 512>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr, kinfo,
+                    rew, fitness, trades, step);
     else
-        launch_path_scan_t<NSM, FR>(nt, n, lds, s, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness, trades,
-                                    step);
+        SGMM_LAUNCH((k_path_scan<NSM, 256, FR, 256>), dim3(n), dim3(nt), lds, s, ep, params, inv_min, cmaps, ctr, kinfo,
+                    rew, fitness, trades, step);
 }
 
 // table + path scan (+ the generation tail when step.st) for one batch
@@ -3232,91 +2572,30 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     EpArrays ep = ep_arrays(eps, arl);
     const bool fr = use_frontier(arl, hidden, eps);
-    if (fr) {
-        ep.fwhole = frontier_whole(eps->n);
-        ep.fnw = kinfo + n_frontier_slots(eps->n);
-    }
+    if (fr) ep.ngrp = frontier_groups(eps->n);
     const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || arl || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (hidden 16 or 32) or the adversary path", eps->max_len,
                  kMaxLen);
     SGMM_REQUIRE(!fr || eps->max_len <= kFrontierMaxLen, "max_len=%d > %lld ticks per episode",
                  eps->max_len, (long long)kFrontierMaxLen);
-    // the fused launch: walks and scans in one kernel (the GA tail included);
-    // its scratch for the tail must fit the 8 KB scan window it aliases
-    // (split episodes' two waves may run on two XCDs: never fused)
-    const bool fused = fr && eps->max_len > 0 && frontier_fused() && ep.fwhole == eps->n &&
-                       (!step.st || step_lds_bytes(kWave, step) <= (size_t)kFusedSel);
     if (fr && eps->max_len > 0) {
-        ProfScope prof(fused ? (vt ? "val_policy_frontier_scan" : "policy_frontier_scan")
-                             : (vt ? "val_policy_frontier" : "policy_frontier"), s);
-        const int nwalk = ep.fwhole + 2 * (eps->n - ep.fwhole);
-        // scanners: the wave slots the walks leave free (3 waves per SIMD), at
-        // least 128 and at most one per episode
-        int nscan = fused ? std::min(eps->n, std::max(128, std::min(1024, 3 * simd_count() - nwalk))) : 0;
-        if (const char* v = std::getenv("SGMM_SCANNERS"); fused && v && std::atoi(v) > 0)
-            nscan = std::min(eps->n, std::atoi(v));
-        const char* pv = std::getenv("SGMM_SCAN_POLL");
-        const int poll = pv && std::atoi(pv) > 0 ? std::atoi(pv) : 1;
-
-        const dim3 grid(nwalk + nscan), block(kWave);
-        FrontierQueue fq{};
-        if (fused) {
-            uint32_t* ctl = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(kinfo) + ws_kinfo_head(eps->n));
-            fq = FrontierQueue{ctl, ctl + 32 * (kXcds + 3), fitness, trades, step, eps->n, nwalk, poll};
-            SGMM_HIP(hipMemsetAsync(ctl, 0, ws_queue(eps->n), s));
-        }
-        FrontierSteal fs{};
-        if (!fused && frontier_steal() && ep.fwhole > 0 && eps->n < (1 << 27)) {
-            uint32_t* ctl = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(kinfo) + ws_kinfo_head(eps->n) +
-                                                        align256(ws_queue(eps->n)));
-            const char* ms = std::getenv("SGMM_STEAL_MAXSEG");
-            const int maxseg = ms ? std::max(1, std::min(kFrontierSegs, std::atoi(ms))) : kFrontierSegs;
-            const char* ev = std::getenv("SGMM_STEAL_EVERY");
-            const char* nc = std::getenv("SGMM_STEAL_CHK");
-            const int every = ev && std::atoi(ev) > 0 ? std::atoi(ev)
-                                                      : std::max(1, nwalk / std::max(1, simd_count() / 4));  // ~1 per CU
-            fs = FrontierSteal{ctl, 1, nwalk, eps->n, maxseg, every, nc && std::atoi(nc) > 0 ? std::atoi(nc) : 3};
-            SGMM_HIP(hipMemsetAsync(ctl, 0, ws_steal(eps->n), s));
-            SGMM_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(ctl + kStActive), nwalk, 1, s));
-            ep.fseg = ctl + kStCtlWords;  // the scan's segment tables
-        }
+        ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
+        const dim3 grid((unsigned)eps->n * (unsigned)ep.ngrp), block(kWave);
         const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
-                              kinfo, rew, fq, fs};
-#define SGMM_FRONTIER(H_, NSI_)                                                                              \
-    do {                                                                                                     \
-        if (fused)                                                                                           \
-            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, true>), grid, block, 0, s, fa);                         \
-        else if (fs.on)                                                                                      \
-            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false, true>), grid, block, 0, s, fa);                  \
-        else                                                                                                 \
-            SGMM_LAUNCH((k_policy_frontier<H_, NSI_, false>), grid, block, 0, s, fa);                        \
-    } while (0)
+                              kinfo, rew};
         if (hidden == 16) {
-            if (nsi <= 5) SGMM_FRONTIER(16, 5);
-            else SGMM_FRONTIER(16, 8);
+            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier<16, 5>), grid, block, 0, s, fa);
+            else SGMM_LAUNCH((k_policy_frontier<16, 8>), grid, block, 0, s, fa);
         } else {
-            if (nsi <= 5) SGMM_FRONTIER(32, 5);
-            else SGMM_FRONTIER(32, 8);
+            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier<32, 5>), grid, block, 0, s, fa);
+            else SGMM_LAUNCH((k_policy_frontier<32, 8>), grid, block, 0, s, fa);
         }
-#undef SGMM_FRONTIER
         SGMM_LAUNCHED();
-        if (fused) {  // the scans (and the GA tail) ran inside; sweep up any left over
-            const int K = step.st ? eps->n / (step.pop_eps > 0 ? step.pop_eps : eps->n) : 0;
-            const dim3 cgrid(std::max(64, std::min(K, 1024)));
-            if (nsi <= 5)
-                SGMM_LAUNCH(k_frontier_cleanup<5>, cgrid, block, 0, s, ep, params, eps->inv_min, cmaps,
-                            reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);
-            else
-                SGMM_LAUNCH(k_frontier_cleanup<8>, cgrid, block, 0, s, ep, params, eps->inv_min, cmaps,
-                            reinterpret_cast<uint32_t*>(ctr), kinfo, rew, fq);
-            SGMM_LAUNCHED();
-            return SGMM_OK;
-        }
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);
-        const bool valu = table_path() == 1;
+        const bool valu = table_valu();
         switch (hidden) {
             case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew); break;
             case 16:

@@ -185,7 +185,7 @@ typedef struct sgmm_ga_state {
     int32_t improved;      /* last generation improved the validation reward */
     int32_t decayed;       /* last generation decayed sigma */
     int32_t patience;      /* 15 (drl_engine.py:155) */
-    int32_t arrivals;      /* internal: workgroup arrival counter of fused launches (0 between launches) */
+    int32_t arrivals;      /* internal: workgroup arrival counter of a launch's generation tail (0 between launches) */
     double  decay;         /* 0.5 (drl_engine.py:156) */
 } sgmm_ga_state;           /* 80 bytes */
 
@@ -340,7 +340,9 @@ int sgmm_rollout_fitness_asked_multi(const sgmm_ticks *ticks, const sgmm_episode
  * master (sgmm_validate_multi) -- instead of validating every individual in
  * the training launch (sgmm_generation_multi).  Four kernel launches;
  * fitness/trades [K*P] (training), val_fitness/val_trades [K].  The workspace
- * must hold the larger of the two batches (sgmm_rollout_workspace_size). */
+ * must hold the larger of the two batches: sgmm_rollout_workspace_bytes(n,
+ * steps, n_inventory, with_adversary) of each, with_adversary = masters_adv !=
+ * NULL for the training batch and 0 for the validation batch. */
 int sgmm_generation_multi_best(const sgmm_ticks *ticks, const sgmm_episodes *train_eps,
                                const sgmm_episodes *val_eps, const sgmm_env_params *params,
                                const sgmm_populations *pops, double *fitness, int32_t *trades,

@@ -17,15 +17,12 @@ pytestmark = [pytest.mark.gpu,
 DEV = torch.device("cuda:0")
 
 
-@pytest.fixture(params=[1, 2, "fused"], ids=["1wave", "2waves", "fused"])
+@pytest.fixture(params=[1, 2, 3, 4], ids=["1wave", "2waves", "3waves", "4waves"])
 def frontier(monkeypatch, request):
-    """The frontier kernel with one wave (64 chunks) or two waves (128 chunks,
-    two independent 64-chunk groups) per episode; "fused": one wave per
-    episode with the path scans inside the launch (scanner waves fed by
-    per-XCD queues, then the cleanup launch)."""
+    """The frontier kernel with the episodes cut into 1-4 chunk groups (one
+    wave of 64 chunks each, chunks of frontier_len(T, groups) ticks)."""
     monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_NW", "1" if request.param == "fused" else str(request.param))
-    monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if request.param == "fused" else "0")
+    monkeypatch.setenv("SGMM_FRONTIER_NW", str(request.param))
 
 
 def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
@@ -87,11 +84,11 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
     assert np.array_equal(fit, wf)
 
 
-@pytest.mark.parametrize("nw", ["", "1", "2", "3"], ids=["default", "1wave", "2waves", "balanced"])
+@pytest.mark.parametrize("nw", ["", "1", "2", "4"], ids=["default", "1wave", "2waves", "4waves"])
 def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
     """From 768 episodes on the frontier kernel is the default: 2100 ragged
-    episodes bit-exact against the oracle (balanced: 972 of them split into
-    two waves, the rest whole, in one launch)."""
+    episodes bit-exact against the oracle, whole or cut into 2 / 4 chunk
+    groups."""
     if nw:
         monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
     lens = 300 + (np.arange(2100) * 37) % 900
@@ -144,24 +141,23 @@ def test_adversary_episodes_have_no_length_cap(sgmm, oracle, H):
 
 def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
     """DRLEngine (device RNG, fused validation) trains identically with the
-    frontier kernel, the frontier kernel with its scans and GA tail fused into
-    the launch (the tail then runs in the cleanup launch), and the table:
+    frontier kernel (whole episodes and 3 chunk groups) and the table:
     histories and final masters."""
     from sgmm_amd import synthetic
     tr = synthetic.bundle_510300(900, seed=51)
     va = synthetic.bundle_510300(200, seed=52)
     st = synthetic.train_stats(tr)
     out = {}
-    for path in ("table", "frontier", "fused"):
-        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path == "fused" else path)
-        monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if path == "fused" else "0")
+    for path in ("table", "frontier", "frontier3"):
+        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path.startswith("frontier") else path)
+        monkeypatch.setenv("SGMM_FRONTIER_NW", "3" if path == "frontier3" else "1")
         torch.manual_seed(7)
         eng = sgmm.DRLEngine(pop_size=40, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / path), hidden_dim=32,
                              rng="device", seed=99, sync_every=4, verbose=False)
         pol, hist = eng.train(tr, va, st, generations=10)
         out[path] = (pol.get_weights().numpy(), hist)
     wa, ha = out["table"]
-    for path in ("frontier", "fused"):
+    for path in ("frontier", "frontier3"):
         wb, hb = out[path]
         for k in ha:
             assert np.array_equal(np.array(ha[k], np.float64), np.array(hb[k], np.float64), equal_nan=True), (path, k)
@@ -169,24 +165,23 @@ def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("val_mode", ["best", "fused"])
-def test_fused_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mode):
-    """Three populations (two assets) trained with the fused frontier launch
-    -- scans by scanner waves, each population's tell (best validation) or
-    whole GA step (fused validation) in the cleanup launch -- equal the table
-    path bit for bit (Env/drl_engine.py:91-171)."""
+def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mode):
+    """Three populations (two assets) trained on the frontier kernel (the
+    scan's last workgroup per population runs its tell, or its whole GA step
+    with fused validation) equal the table path bit for bit
+    (Env/drl_engine.py:91-171)."""
     import _shard_ranks as R
     tr, va, st = R.multi_workload()
     out = {}
-    for path in ("table", "fused"):
-        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path == "fused" else "table")
-        monkeypatch.setenv("SGMM_FRONTIER_FUSED", "1" if path == "fused" else "0")
+    for path in ("table", "frontier"):
+        monkeypatch.setenv("SGMM_TABLE_PATH", path)
         m = R.multi_engines(sgmm, 30, False, str(tmp_path / path), val_mode, dist=False)
         out[path] = R.multi_result(m, m.train(tr, va, st, generations=8))
     for key in out["table"]:
-        assert np.array_equal(out["table"][key], out["fused"][key], equal_nan=True), key
+        assert np.array_equal(out["table"][key], out["frontier"][key], equal_nan=True), key
 
 
-@pytest.mark.parametrize("nw", ["1", "2"], ids=["1wave", "2waves"])
+@pytest.mark.parametrize("nw", ["1", "2", "4"], ids=["1wave", "2waves", "4waves"])
 def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
     """Above 1024 episodes the path scan is one wave per episode (1024-tick
     windows of a 256-thread layout run by 64 lanes): chunk lengths from 4 to
@@ -200,57 +195,3 @@ def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=51, sigma=0.3)
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
-
-
-def test_frontier_tick_handoffs_equal_whole(sgmm, oracle, monkeypatch):
-    """Tick hand-offs (SGMM_FRONTIER_STEAL=1, opt-in): a walk that sees a
-    waiting helper hands the second half of its remaining ticks over as a new
-    segment of its chunks (every start state tracked), so the episode's
-    records come in up to 4 segments that the scan chains in tick order.  On
-    a batch big enough to have helpers (2560 episodes; every finished wave a
-    helper, eight checks per segment) the results equal the walks without
-    hand-offs bit for bit, and hand-offs did happen."""
-    from sgmm_amd import synthetic
-    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_NW", "1")
-    monkeypatch.setenv("SGMM_FRONTIER_FUSED", "0")
-    P, T, H = 2560, 4560, 32  # 72-tick chunks: a half-way check leaves >= 16 ticks
-    b = synthetic.bundle_510300(T, seed=41)
-    st = synthetic.train_stats(b)
-    # a spread of sigmas: policies that rarely fill keep their paths apart (heavy walks)
-    pop = torch.cat([synthetic.population(P // 4, H, sigma=s, seed=42 + k)
-                     for k, s in enumerate((0.05, 0.2, 0.5, 1.0))])
-    ticks = sgmm.TickStore()
-    seg = ticks.add(b, st)
-    ticks.to(DEV)
-    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.001, tick_size=0.001)], DEV)
-    lens = np.full(P, T)
-    lens[::7] = T - 124  # ragged lengths
-    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P)).to(DEV)
-    eng = sgmm.RolloutEngine(DEV)
-    mm = pop.to(DEV)
-    monkeypatch.setenv("SGMM_FRONTIER_STEAL", "0")
-    f0, t0 = (x.cpu().numpy() for x in eng.fitness(ticks, eb, params, mm, H))
-    monkeypatch.setenv("SGMM_FRONTIER_STEAL", "1")
-    monkeypatch.setenv("SGMM_STEAL_EVERY", "1")
-    monkeypatch.setenv("SGMM_STEAL_CHK", "8")
-    f1, t1 = (x.cpu().numpy() for x in eng.fitness(ticks, eb, params, mm, H))
-    torch.cuda.synchronize()
-    # the segment tables (workspace layout of sgmm_rollout_workspace_bytes: chunk maps,
-    # trade counts, merge info + wave counts, the fused queues, then the hand-off area)
-    def a256(x):
-        return (x + 255) & ~255
-    n, steps = P, int(lens.sum())
-    nchunk = steps // 64 + n + 1
-    off = a256(max(nchunk, n * 256) * 8) + a256(max(nchunk * 8, n * 256 * 32)) + a256((n * 256 + n) * 4) + \
-        a256(4 * 32 * 11 + 4 * 8 * n)
-    segs = eng._ws[off + 640:off + 640 + 16 * n].view(torch.int32).cpu().numpy().reshape(n, 4)[:, 0]
-    assert (segs > 1).sum() > 0, "no hand-off happened"
-    assert np.array_equal(t0, t1) and np.array_equal(f0, f1)
-    # and the first episodes against the oracle
-    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
-    k = 48
-    wf, wt = oracle.evaluate_batch(pop[:k].numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(k), None,
-                                   np.zeros(k), lens[:k], np.zeros(k), [oracle.params(phi=0.001, tick=0.001)],
-                                   n_threads=8)
-    assert np.array_equal(wt, t1[:k]) and np.array_equal(wf, f1[:k])

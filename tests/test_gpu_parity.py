@@ -282,11 +282,12 @@ def test_scan_ragged_lengths(golden, sgmm, oracle):
             assert trd[i].item() == t and fit[i].item() == f, (H, i)
 
 
-@pytest.mark.parametrize("path", ["valu", "v2", "v3", "v3i", "frontier"])
+@pytest.mark.parametrize("path", ["valu", "table", "frontier"])
 def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
-    """Every policy-table kernel -- VALU, the f32-MFMA table (v2 schedule, v3
-    with one / two accumulator sets) and the frontier kernel -- reproduces the
-    oracle's canonical fma chains bit for bit (the MFMA k-order equals the chain)."""
+    """Every policy kernel -- the VALU table, the f32-MFMA table (v3 schedule;
+    k_policy_table_mfma with the adversary and for H = 64) and the frontier
+    kernel -- reproduces the oracle's canonical fma chains bit for bit (the MFMA
+    k-order equals the chain)."""
     monkeypatch.setenv("SGMM_TABLE_PATH", path)
     eps = list(episodes_from_fixture(golden("g2_synthetic.npz")))
     eps += _synthetic_batch(sgmm, 4, 1000, 32, seed=77, sigma=0.4)
