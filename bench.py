@@ -346,8 +346,9 @@ def main():
     if tab:
         achieved = steps_per_launch * fl / (tab["avg_us"] * 1e-6) / 1e12
         traffic = None
-        if pmc and pmc.get("kernels", {}).get(kname):
-            traffic = pmc["kernels"][kname].get("hbm_bytes_per_launch")
+        pk = next((k for k in (pmc or {}).get("kernels", {}) if k == kname or k.startswith(kname + "<")), None)
+        if pk:
+            traffic = pmc["kernels"][pk].get("hbm_bytes_per_launch")
         note = ("algorithmic = one policy forward per env-step ("
                 + ("training" if best_val else "training + validation") + " ticks of one launch). "
                 + ("k_policy_frontier evaluates only the inventory states a chunk's paths occupy (about 1.2-1.35 per "

@@ -831,6 +831,7 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
+constexpr int kFrPrioExtra = 160;      // a walk's issue priority from 0.625 extra slots per tick on average
 constexpr int kFrontierMaxWaves = 4;   // waves (64-chunk groups) per episode
 constexpr int kFrontierRecs = kFrontierLanes * kFrontierMaxWaves;  // chunk records per episode: e * 256 + c
 constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
@@ -851,18 +852,14 @@ constexpr int kFrontierPad = 4 * kFrontierRecs + 16;  // plane rows per episode 
 __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
     return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
 }
-// Within a group's block, the reward of chunk (lane) l at tick offset u: the
-// 64 chunks' 4-tick groups side by side -- a walk's store of one tick is one
-// coalesced 2 KB span (each 128-byte line complete after 4 ticks), a scan
-// thread's 4 ticks are 32 contiguous bytes (one cache line, two 16-byte loads
-// instead of four 8-byte loads on four lines).  SGMM_PLANE1: round 2's rows
-// (tick offset u, lane l at u * 64 + l).
+// Within a group's block, the reward of chunk (lane) l at tick offset u: rows
+// of the 64 chunks at one tick offset (u * 64 + l) -- a walk's store of one
+// tick is one 512-byte row per plane, four whole 128-byte lines.  (Round 3's
+// 4-tick groups, ((u >> 2) * 64 + l) * 4 + (u & 3), gave the scan one line per 4
+// ticks but left lines part-written across ticks: 254 vs 185 MB written per
+// config-3 launch, same time: profiles/r04_ab/r04l*.)
 __host__ __device__ __forceinline__ int64_t frontier_row(int u, int l) {
-#ifdef SGMM_PLANE1
     return (int64_t)u * kFrontierLanes + l;
-#else
-    return ((int64_t)(u >> 2) * kFrontierLanes + l) * 4 + (u & 3);
-#endif
 }
 
 // ------------------------------------------------------------------ exact ordered sum
@@ -1385,35 +1382,13 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
                     const uint32_t ki = kin[c];
                     const int kc = (int)(ki & 0x1FFFFFFFu);
                     const int64_t pst = start[c], pp0 = ki >> 29;
-#ifdef SGMM_PLANE1
                     const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
-                                       c % kFrontierLanes;
+                                       frontier_row(u, c % kFrontierLanes);
 #pragma unroll
                     for (int j = 0; j < kSumTpt; ++j) {
                         const int jj = min(j, n - 1 - i0);
-                        r[g][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)(u + jj) * kFrontierLanes];
+                        r[g][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)jj * kFrontierLanes];
                     }
-#else
-                    // the chunk's 4 ticks u .. u + 3 are 32 contiguous bytes (frontier_row)
-                    const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
-                                       frontier_row(u, c % kFrontierLanes);
-                    // one plane for the 4 ticks unless the paths merge inside them
-                    double2 a0{0.0, 0.0}, a1{0.0, 0.0}, b0{0.0, 0.0}, b1{0.0, 0.0};
-                    if (u < kc) {
-                        const double2* pa = reinterpret_cast<const double2*>(rew + pst * ep.rs + rb);
-                        a0 = pa[0];
-                        a1 = pa[1];
-                    }
-                    if (u + kSumTpt - 1 >= kc) {
-                        const double2* pb = reinterpret_cast<const double2*>(rew + pp0 * ep.rs + rb);
-                        b0 = pb[0];
-                        b1 = pb[1];
-                    }
-                    r[g][0] = u >= kc ? b0.x : a0.x;
-                    r[g][1] = u + 1 >= kc ? b0.y : a0.y;
-                    r[g][2] = u + 2 >= kc ? b1.x : a1.x;
-                    r[g][3] = u + 3 >= kc ? b1.y : a1.y;
-#endif
                 } else {
                     const double* __restrict__ src = rew + (int64_t)start[(w0 + i0) / kChunk] * ep.rs + so + w0 + i0;
 #pragma unroll
@@ -1603,6 +1578,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #endif
     int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
+    int fr_extra = 0;
 #pragma unroll 1
     for (int tt = 0; tt < CL; ++tt) {
 #ifdef SGMM_STAMPS_PHASE
@@ -1688,6 +1664,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         }
         const bool any0 = __ballot(fmask != 0u) != 0ull;
         const int nx = (etot + kWave - 1) / kWave;
+        // a walk whose ticks have needed extra slots for a while (its paths stay
+        // apart: a heavy walk, the launch's tail) takes the SIMD's issue
+        // priority over the light walks beside it (config 3: policy kernel
+        // 560-571 -> 533 us at thresholds 128 and 192, profiles/r04_ab)
+        fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
+#ifndef SGMM_NO_FR_PRIO
+        if ((tt & 7) == 7) {
+            if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
 #ifdef SGMM_STAMPS
         lite_sl += (any0 ? 1 : 0) + nx;
         if (tt == 7) lite_s8 = lite_sl;    // slots run in the first 8 / 16 ticks (heaviness probes)
@@ -2425,8 +2412,8 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
 
 // Chunk groups per episode in the frontier kernel (one wave each).  A walk's
 // time is set by its serial chain of ticks, not by its SIMD's load, so when the
-// launch has fewer walks than the chip has wave slots (3 per SIMD) the
-// episodes are cut into 2-4 groups of 64 chunks of proportionally fewer ticks;
+// launch has fewer than two walks per SIMD the episodes are cut into 2-4
+// groups of 64 chunks of proportionally fewer ticks;
 // each extra group pays for tracking every start state of its chunks until
 // their paths merge.  SGMM_FRONTIER_NW=1..4 forces the count.
 static int simd_count() {
@@ -2446,7 +2433,10 @@ static int32_t frontier_groups(int32_t n) {
         if (g >= 1 && g <= kFrontierMaxWaves) return g;
     }
     if (n <= 0) return 1;
-    const int64_t slots = 3LL * simd_count();
+    // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
+    // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups; 256 and 64
+    // episodes: 4 groups fastest, profiles/r04_ab)
+    const int64_t slots = 2LL * simd_count();
     return (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierMaxWaves, slots / n));
 }
 

@@ -15,7 +15,7 @@ import numpy as np
 H, K, P = 32, 5, 512
 MODE = sys.argv[1] if len(sys.argv) > 1 else "time"
 if MODE == "slots":
-    os.environ["SGMM_LIB"] = str(ROOT / "tools/diag/libsgmm_stamps.so")
+    os.environ["SGMM_LIB"] = str(ROOT / "tools/stamps/libsgmm_stamps.so")
     os.environ["SGMM_FRONTIER_NW"] = "1"
 import torch
 import sgmm_pkg

@@ -10,7 +10,7 @@ import os
 import sys
 from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
-os.environ["SGMM_LIB"] = str(ROOT / "tools/diag/libsgmm_stamps.so")
+os.environ["SGMM_LIB"] = str(ROOT / "tools/stamps/libsgmm_stamps.so")
 sys.path.insert(0, str(ROOT))
 import numpy as np
 import torch

@@ -1,7 +1,7 @@
 """Diagnostic: sgmm_ordered_sum on the bench workload's real selected rewards
 (oracle trace of one P=64 bench episode, H=16, T=3600).  Prints us per call
 (HIP events) with the stamped library
-(SGMM_LIB=tools/diag/libsgmm_stamps.so) also the v2 phase cycles."""
+(SGMM_LIB=tools/stamps/libsgmm_stamps.so) also the v2 phase cycles."""
 import ctypes
 import os
 import sys

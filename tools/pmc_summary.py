@@ -11,6 +11,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 KINDS = ("policy_table", "policy_frontier", "path_scan", "ga_step", "rollout_direct", "ordered_sum")
@@ -19,7 +20,8 @@ KINDS = ("policy_table", "policy_frontier", "path_scan", "ga_step", "rollout_dir
 def kind(name):
     for k in KINDS:
         if k in name:
-            return k
+            m = re.search(k + r"(<[^>]*>)?", name)
+            return k + (m.group(1).replace(" ", "") if m and m.group(1) else "")
     return name.split("(")[0][:60]
 
 

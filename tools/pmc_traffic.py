@@ -10,6 +10,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 KIND = (("policy_table", "policy_table"), ("policy_frontier", "policy_frontier"), ("path_scan", "path_scan"), ("ga_step", "ga_step"),
@@ -17,9 +18,12 @@ KIND = (("policy_table", "policy_table"), ("policy_frontier", "policy_frontier")
 
 
 def kind(name):
+    """'policy_frontier<32, 5>' style key: family plus template arguments, so the
+    main and validation launches of one family are kept apart."""
     for key, k in KIND:
         if key in name:
-            return k
+            m = re.search(key + r"(<[^>]*>)?", name)
+            return k + (m.group(1).replace(" ", "") if m and m.group(1) else "")
     return None
 
 
@@ -37,6 +41,9 @@ def main(fd, wd, out):
     fetch = load(fd, "FETCH_SIZE")
     write = load(wd, "WRITE_SIZE")
     res = {"correction": "read bytes = 2 x FETCH_SIZE (gfx950 half-count on wide reads); KiB units",
+           "calibration": "the x2 read correction and exact WRITE_SIZE are calibrated for 16-B-per-lane streams; "
+                          "the frontier stores and scan loads are 8 B per lane (uncalibrated), so reads may be "
+                          "over-stated up to 2x",
            "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = sum(fetch[k]) / len(fetch[k]) if fetch.get(k) else 0.0

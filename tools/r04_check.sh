@@ -1,6 +1,5 @@
 #!/bin/bash
-# round 4: GPU suite + smoke + config-3 bench line, then the config-5 (1 of 8)
-# and config-4 (1 of 4) shard lines at 1-4 frontier chunk groups
+# round 4: GPU suite + smoke, then the bench lines of every config and shard shape
 set -o pipefail
 cd "$(dirname "$0")/.."
 tag=${1:-r04}
@@ -9,11 +8,16 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
   || { tail -30 gpurun_out/$tag/tests.log; exit 1; }
 tail -1 gpurun_out/$tag/tests.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -1 || exit 1
-timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/$tag/c3.json 2> gpurun_out/$tag/c3.err \
-  || { tail -20 gpurun_out/$tag/c3.err; exit 1; }
-python tools/bench_summary.py gpurun_out/$tag/c3.json
-for nw in 1 2 3 4; do
-  SGMM_FRONTIER_NW=$nw timeout -k 10 300 python -u bench.py --config 5 --shard-of 8 --steps 20 --warmup 5 --no-cpu-baseline \
-    > gpurun_out/$tag/c5s8_nw$nw.json 2> gpurun_out/$tag/c5s8_nw$nw.err || { tail -20 gpurun_out/$tag/c5s8_nw$nw.err; exit 1; }
-  echo "c5 1/8 nw=$nw"; python tools/bench_summary.py gpurun_out/$tag/c5s8_nw$nw.json
-done
+bench() {  # name env... (BARGS: bench arguments)
+  local name=$1; shift
+  env "$@" timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 $BARGS > gpurun_out/$tag/$name.json 2> gpurun_out/$tag/$name.err \
+    || { tail -20 gpurun_out/$tag/$name.err; exit 1; }
+  python tools/bench_summary.py gpurun_out/$tag/$name.json
+}
+BARGS="" bench c3 SGMM_X=0
+BARGS="--no-cpu-baseline --config 5 --shard-of 8" bench c5s8 SGMM_X=0
+BARGS="--no-cpu-baseline --config 4" bench c4 SGMM_X=0
+BARGS="--no-cpu-baseline --config 4 --shard-of 4" bench c4s4 SGMM_X=0
+BARGS="--no-cpu-baseline --config 2" bench c2 SGMM_X=0
+BARGS="--no-cpu-baseline --config 6" bench c6 SGMM_X=0
+BARGS="--no-cpu-baseline --config 7" bench c7 SGMM_X=0
