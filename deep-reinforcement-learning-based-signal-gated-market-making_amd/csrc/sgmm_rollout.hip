@@ -856,8 +856,8 @@ __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
 // of the 64 chunks at one tick offset (u * 64 + l) -- a walk's store of one
 // tick is one 512-byte row per plane, four whole 128-byte lines.  (Round 3's
 // 4-tick groups, ((u >> 2) * 64 + l) * 4 + (u & 3), gave the scan one line per 4
-// ticks but left lines part-written across ticks: 254 vs 185 MB written per
-// config-3 launch, same time: profiles/r04_ab/r04l*.)
+// ticks but left lines part-written across ticks: 254 vs 155 MB written per
+// config-3 launch, profiles/r03_pmc_traffic_c3.json vs r04_pmc_traffic_c3.json.)
 __host__ __device__ __forceinline__ int64_t frontier_row(int u, int l) {
     return (int64_t)u * kFrontierLanes + l;
 }
@@ -896,7 +896,8 @@ constexpr int kSumTpt = 4;          // rewards gathered per path-scan thread
 constexpr int kScanThreads = 1024;  // path-scan workgroup
 constexpr int kScanWin = kScanThreads * kSumTpt;
 constexpr int kScanAt1024 = 256;  // path-scan workgroup: 1024 threads up to this many episodes,
-constexpr int kScanAt512 = 1024;  // 512 up to this many, 256 above
+constexpr int kScanAt512 = 512;   // 512 up to this many, one wave above
+constexpr int kScanArlAt1024 = 1024;  // adversary path scan: 1024 threads up to this many, kScanBlock above
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
 static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
@@ -2395,8 +2396,10 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
 // SGMM_FRONTIER_MIN_EPS moves the threshold.  Measured crossover (one rank's
 // shard of config 5, H = 32, 3600 ticks, per generation, profiles/r03_c5_shard*):
 // 256 episodes table 235 / frontier 363 us, 512: 365 / 435, 1024: 633 / 525,
-// 2048: 1078 / 572 -- the lines cross near 700 episodes.
-constexpr int kFrontierMinEps = 768;
+// 2048: 1078 / 572 -- the lines crossed near 700 episodes.  With 2-4 chunk
+// groups per episode (round 4, training launch alone, profiles/r04_ab/r04m_*,
+// r04n_*): 256 episodes table 167 / frontier 162 us, 512: 255-263 / 195-204.
+constexpr int kFrontierMinEps = 512;
 static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     if (arl || (hidden != 16 && hidden != 32)) return false;
     if (eps->max_len > kMaxLen) return true;
@@ -2505,9 +2508,10 @@ static int scan_threads(int64_t n) {
         const int t = std::atoi(v);
         if (t == 64 || t == 256 || t == 512 || t == 1024) return t;
     }
-    // beyond 1024 episodes one-wave workgroups: the exact-sum walk is serial,
-    // so ~15 episodes resident per CU beat 4 wider workgroups (config 3:
-    // 193 -> 145 us per scan, tools/gpu_sc1.sh)
+    // beyond 512 episodes one-wave workgroups: the exact-sum walk is serial,
+    // so many episodes resident per CU beat fewer wider workgroups (config 3:
+    // 193 -> 145 us per scan, tools/gpu_sc1.sh; config 5's 1-of-8 shard, 1024
+    // episodes: 110 -> 74 us, profiles/r04_ab/r04k_*)
     return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : kWave);
 }
 
@@ -2607,7 +2611,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     if (arl) {
         // 16-wave workgroups while one per CU fits (a 4096-tick segment is one
         // exact-sum window), 4-wave ones beyond
-        const int nt = eps->n <= kScanAt512 ? kScanThreads : kScanBlock;
+        const int nt = eps->n <= kScanArlAt1024 ? kScanThreads : kScanBlock;
         size_t lds = arl_scan_lds(ns);
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
         if (nt == kScanThreads)
