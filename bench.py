@@ -346,7 +346,10 @@ def main():
     if tab:
         achieved = steps_per_launch * fl / (tab["avg_us"] * 1e-6) / 1e12
         traffic = None
-        pk = next((k for k in (pmc or {}).get("kernels", {}) if k == kname or k.startswith(kname + "<")), None)
+        # the training launch's entry (keys carry the template: policy_table_mfma<32,5,true>; the
+        # validation launch's smaller entry of the same family is not it)
+        cands = [k for k in (pmc or {}).get("kernels", {}) if k.startswith(kname)]
+        pk = max(cands, key=lambda k: pmc["kernels"][k].get("hbm_bytes_per_launch") or 0) if cands else None
         if pk:
             traffic = pmc["kernels"][pk].get("hbm_bytes_per_launch")
         note = ("algorithmic = one policy forward per env-step ("

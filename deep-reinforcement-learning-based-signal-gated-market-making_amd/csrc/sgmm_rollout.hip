@@ -551,13 +551,31 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? 5 : ((ARL && H <= 32) ? 3 : 1)
                 traded |= (uint32_t)(so.fill_buy | so.fill_sell) << si;
                 rl[si * kWave + lane] = so.reward;
             } else {
+                // the 4 (previous fills) states of this inventory differ only by the
+                // adversary's delta (wave-uniform: one adversary per episode); states
+                // whose delta equals an earlier one's take that step's result
+                // (adv_scale 1: deltas in {-1, 0, 1}, mostly shared)
+                int32_t dac[4], dbc[4], fc[4];
+                double rc[4];
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const int s = 4 * si + c;
-                    const StepOut so = ftp_step(p, inv, oa + lut0[s], ob + lut1[s], mid, ask, bid,
-                                                bmax, smin);
-                    fw |= (uint64_t)(so.fill_buy | (so.fill_sell << 1)) << (2 * s);
-                    rew[s * ep.rs + row] = so.reward;  // per-state planes (SoA): coalesced rows
+                    dac[c] = __builtin_amdgcn_readfirstlane(lut0[s]);
+                    dbc[c] = __builtin_amdgcn_readfirstlane(lut1[s]);
+                    int dup = -1;
+#pragma unroll
+                    for (int c2 = c - 1; c2 >= 0; --c2)
+                        if (dac[c2] == dac[c] && dbc[c2] == dbc[c]) dup = c2;
+                    if (dup < 0) {
+                        const StepOut so = ftp_step(p, inv, oa + dac[c], ob + dbc[c], mid, ask, bid, bmax, smin);
+                        rc[c] = so.reward;
+                        fc[c] = so.fill_buy | (so.fill_sell << 1);
+                    } else {
+                        rc[c] = dup == 0 ? rc[0] : (dup == 1 ? rc[1] : rc[2]);
+                        fc[c] = dup == 0 ? fc[0] : (dup == 1 ? fc[1] : fc[2]);
+                    }
+                    fw |= (uint64_t)fc[c] << (2 * s);
+                    rew[s * ep.rs + row] = rc[c];  // per-state planes (SoA): coalesced rows
                 }
             }
         }
@@ -899,6 +917,7 @@ constexpr int kScanAt1024 = 256;  // path-scan workgroup: 1024 threads up to thi
 constexpr int kScanAt512 = 512;   // 512 up to this many, one wave above
 constexpr int kScanArlAt1024 = 1024;  // adversary path scan: 1024 threads up to this many, kScanBlock above
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
+constexpr int32_t kZeroRun = INT32_MAX;  // a block's prediction: all its values are +-0.0
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
 static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
 
@@ -1041,7 +1060,15 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
         // added the reference way
         const bool edge = fast && (ma > 0 ? (ma + mx > kMHi - kEdge || ma + mn < kMLo + kEdge)
                                           : (ma + mn < -kMHi + kEdge || ma + mx > -kMLo - kEdge));
-        const int32_t be = (fast && !bad && !edge) ? eb : INT32_MIN;
+        // a block of exact zeros (either sign) leaves any S unchanged (S is
+        // never -0.0: the sum starts at +0.0 and round-to-nearest cancels to
+        // +0.0), whatever its binade -- runs of them are skipped whole, which is
+        // what keeps an idle individual's walk (S = 0 for the whole episode:
+        // every block was a fallback) as short as a trading one's
+        bool allz = true;
+#pragma unroll
+        for (int j = 0; j < kSumBlk; ++j) allz &= r[j] == 0.0;
+        const int32_t be = allz ? kZeroRun : (fast && !bad && !edge) ? eb : INT32_MIN;
         // block sums -> wave-local exclusive prefix zl
         const uint64_t zinc = wave_scan_add((uint64_t)P);
         const int64_t zl = (int64_t)(zinc - (uint64_t)P);
@@ -1132,9 +1159,11 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
 #endif
                 const SumRec rn = L.rec[min(pos + 1, NB - 1)];
                 const SumRec rj = L.rec[min(cur.rend, NB - 1)];
-                const bool ok = ib && cur.be == e &&
+                // (a zero run is skipped unless S is -0.0: only the API's init can make it so)
+                const bool ok = (cur.be == kZeroRun && (ib || __double_as_longlong(S) != INT64_MIN)) ||
+                                (ib && cur.be == e &&
                                 (M > 0 ? (M + cur.mn >= kMLo && M + cur.mx <= kMHi)
-                                       : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi));
+                                       : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi)));
                 const int64_t Mj = M + cur.dsum;
                 const int pj = cur.rend;
                 if (!ok) {  // this block the reference way (the last block padded with -0.0)

@@ -86,7 +86,7 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
 
 @pytest.mark.parametrize("nw", ["", "1", "2", "4"], ids=["default", "1wave", "2waves", "4waves"])
 def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
-    """From 768 episodes on the frontier kernel is the default: 2100 ragged
+    """From 512 episodes on the frontier kernel is the default: 2100 ragged
     episodes bit-exact against the oracle, whole or cut into 2 / 4 chunk
     groups."""
     if nw:
@@ -109,6 +109,27 @@ def test_frontier_default_selection_config5_shard(sgmm, oracle):
     _lib.profile_enable(True)
     try:
         fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=53, sigma=0.1)
+        kernels = _lib.profile_read()
+    finally:
+        _lib.profile_enable(False)
+    assert "policy_frontier" in kernels, kernels
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
+@pytest.mark.parametrize("n", [512, 600], ids=["c5_16ranks", "600"])
+def test_frontier_default_selection_small_shards(sgmm, oracle, n):
+    """Config 5's shard on 16 GPUs (2 x 256 individuals = 512 episodes of 3600
+    ticks, H = 32: 4 chunk groups per episode, 512-thread scan) and 600
+    episodes (3 groups, one-wave scan) run the frontier kernel by default
+    (profiles/r04_ab/r04m_*: 512 episodes 195-204 us frontier vs 255-263 us
+    table); bit-exact against the oracle."""
+    from sgmm_amd import _lib
+    lens = 3600 - (np.arange(n) % 7) * 4
+    _lib.profile_read()
+    _lib.profile_enable(True)
+    try:
+        fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=57, sigma=0.1)
         kernels = _lib.profile_read()
     finally:
         _lib.profile_enable(False)
@@ -183,7 +204,7 @@ def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mod
 
 @pytest.mark.parametrize("nw", ["1", "2", "4"], ids=["1wave", "2waves", "4waves"])
 def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
-    """Above 1024 episodes the path scan is one wave per episode (1024-tick
+    """Above 512 episodes the path scan is one wave per episode (1024-tick
     windows of a 256-thread layout run by 64 lanes): chunk lengths from 4 to
     past 512 ticks, ragged last windows and chunks, both chunk groups of split
     episodes -- bit-exact against the oracle."""

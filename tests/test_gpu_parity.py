@@ -206,10 +206,11 @@ def test_bench_config_population(sgmm, oracle):
 
 
 @pytest.mark.parametrize("caps", [(2, -2), (3, -4)], ids=["5states", "8states"])
-@pytest.mark.parametrize("n_ep", [600, 1100])
+@pytest.mark.parametrize("n_ep", [400, 600, 1100])
 def test_many_episode_scan(sgmm, oracle, n_ep, caps):
-    """More than 256 / 1024 episodes take the 8- / 4-wave path scan (2048- /
-    1024-tick windows): ragged lengths around their window boundaries, every
+    """More than 256 / 512 episodes take the 8-wave / one-wave path scan (2048- /
+    1024-tick windows; 400 episodes run the table, 600 and 1100 the frontier
+    kernel): ragged lengths around their window boundaries, every
     episode bit-exact; with 5 inventory states (the default caps) and with 8
     (i_max=3, i_min=-4: the NSM=8 scan instantiations)."""
     i_max, i_min = caps
@@ -331,7 +332,15 @@ def _sum_cases():
             ("edge_down", 2.0 + 2e-10, np.full(5000, -1e-13) + rng.normal(0, 1e-16, 5000)),
             ("edge_neg", -1.0 + 2e-10, np.full(5000, -1e-13)),
             ("zigzag", 0.0, np.tile([1e-3, -1e-3, 2e-3, -2e-3 + 1e-19], 1500)),
-            ("exact_edges", 0.5 - 2.0 ** -40, np.full(4100, 2.0 ** -50))]
+            ("exact_edges", 0.5 - 2.0 ** -40, np.full(4100, 2.0 ** -50)),
+            # runs of exact zeros (an idle individual's rewards) are skipped whole by the walk
+            ("idle", 0.0, np.zeros(4560)),
+            ("idle_negzero", -0.0, np.zeros(100)),
+            ("negzero_runs", -0.0, np.concatenate([-np.zeros(40), np.zeros(40), -np.zeros(40)])),
+            ("zero_runs", 0.0, np.concatenate([np.zeros(2000), env_like[:500], -np.zeros(3000), env_like[:33],
+                                               np.zeros(17), [1e-300], np.zeros(1000)])),
+            ("zero_runs_inf", 0.0, np.concatenate([np.zeros(500), [np.inf], np.zeros(600), [1.0]])),
+            ("zero_runs_init", 123.25, np.concatenate([np.zeros(1100), env_like[:300], np.zeros(5000)]))]
 
 
 @pytest.mark.parametrize("name,init,x", _sum_cases(), ids=[c[0] for c in _sum_cases()])

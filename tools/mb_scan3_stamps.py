@@ -67,3 +67,13 @@ t4, t5 = h[:, 4], h[:, 5]
 m = (t5 > t4) & (t4 > 0)
 if m.any():
     print("  tail (last arrivers):", [(int(e), int(t5[e] - t4[e])) for e in np.where(m)[0][:8]])
+# the slowest episodes: what distinguishes them (walk iterations, fallbacks, gather / sum cycles, windows)
+o = np.argsort(tot)[::-1]
+print("  slowest episodes: (e, entry->end, gather, sum, walk iters, fallbacks, windows)")
+for e in o[:12]:
+    print("   ", int(e), int(tot[e]), int(g[e]), int(sm[e]), int(h[e, 13]), int(h[e, 14]), int(h[e, 15]))
+for q in (50, 90, 99):
+    sel_ = tot >= np.percentile(tot, q)
+    print(f"  >= p{q}: mean fallbacks {h[sel_, 14].mean():.1f} iters {h[sel_, 13].mean():.1f} sum {sm[sel_].mean():.0f} gather {g[sel_].mean():.0f}")
+print("  corr(entry->end, fallbacks) %.2f, (.., iters) %.2f, (.., gather) %.2f" % (
+    np.corrcoef(tot, h[:, 14])[0, 1], np.corrcoef(tot, h[:, 13])[0, 1], np.corrcoef(tot, g)[0, 1]))

@@ -20,7 +20,7 @@ KINDS = ("policy_table", "policy_frontier", "path_scan", "ga_step", "rollout_dir
 def kind(name):
     for k in KINDS:
         if k in name:
-            m = re.search(k + r"(<[^>]*>)?", name)
+            m = re.search(k + r"(\w*<[^>]*>)?", name)
             return k + (m.group(1).replace(" ", "") if m and m.group(1) else "")
     return name.split("(")[0][:60]
 

@@ -22,7 +22,7 @@ def kind(name):
     main and validation launches of one family are kept apart."""
     for key, k in KIND:
         if key in name:
-            m = re.search(key + r"(<[^>]*>)?", name)
+            m = re.search(key + r"(\w*<[^>]*>)?", name)
             return k + (m.group(1).replace(" ", "") if m and m.group(1) else "")
     return None
 
