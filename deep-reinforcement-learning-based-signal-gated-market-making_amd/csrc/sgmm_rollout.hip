@@ -2060,6 +2060,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
     const uint64_t* __restrict__ F = fills + so;
     const int tid = threadIdx.x;
     if (tid == 0) red_trades = 0;
+    SGMM_STAMP(e, 0);
     int carry = (-inv_min) << 2;  // the state entering the segment (episode start: inventory 0, no fills)
     int my_trades = 0;
     double total = 0.0;
@@ -2068,6 +2069,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         const int segch = (segn + kChunk - 1) / kChunk;
         for (int i = tid; i < segn; i += NT) fl[i] = F[seg0 + i];
         __syncthreads();
+        SGMM_STAMP(e, 1);
         // chunk k's transducer from start state s (padded ticks: none, the walk stops at the chunk's end)
         for (int i = tid; i < segch * ns; i += NT) {
             const int k = i / ns;
@@ -2089,6 +2091,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
             tr[i] = (uint8_t)cnt;
         }
         __syncthreads();
+        SGMM_STAMP(e, 6);
         // jm[k][s] = state after chunks k-2^r+1 .. k from state s at chunk k-2^r+1's start
         int cur = 0;
         for (int d = 1; d < segch; d <<= 1) {
@@ -2109,6 +2112,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
             my_trades += tr[k * ns + st];
         }
         __syncthreads();
+        SGMM_STAMP(e, 7);
         carry = pre[(segch - 1) * ns + carry];
         if (tid < segch) {  // chunk tid's state path
             int st = start[tid];
@@ -2126,8 +2130,10 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
             }
         }
         __syncthreads();  // the codes are dead: sel takes their place
+        SGMM_STAMP(e, 11);
         for (int i = tid; i < segn; i += NT) sel[i] = rew[(int64_t)stt[i] * ep.rs + so + seg0 + i];
         __syncthreads();
+        SGMM_STAMP(e, 12);
         for (int k = 0; k < segn; k += 4 * NT)  // windows of 4 values per thread
             total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L);
     }
@@ -2141,6 +2147,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         if (tr_ == 0) total -= params[ep.param[e]].idle_penalty;
         store_record(fitness, trades_out, e, total, tr_);
     }
+    SGMM_STAMP(e, 3);
     if (step.st) generation_tail(step, fitness, trades_out, lds, &red_trades, e, (int)gridDim.x);
 }
 
