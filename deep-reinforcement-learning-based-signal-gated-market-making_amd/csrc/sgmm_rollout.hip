@@ -990,7 +990,14 @@ struct SumLds {
 // and a barrier has passed; returns S + sel[0] + ... + sel[n-1] in sequential
 // float64 order in every thread.  S must be the same in every thread.  Ends
 // with a barrier (sel may then be refilled).
-template <int NT>
+// STREAK: a block without a prediction takes the rest of its run with it (one
+// loop of reference additions, no walk step per block).  It shortens the
+// walks of the episodes with long fallback streaks -- the slowest ones -- and
+// costs the others a little: on for the one-wave and the adversary scans
+// (config 3 scan 129 -> 115 us, config 4 53.3 -> 51.6 us), off for the
+// 512/1024-thread scans of small batches (config 2 scan 17.8 -> 19.3 us with
+// it; profiles/r04_ab/r04u*).
+template <int NT, bool STREAK = (NT == 4 * kWave)>
 __device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L) {
     static_assert(NT % (4 * kWave) == 0, "whole block waves");
     constexpr int NB = NT / 4;         // 16-value blocks per window
@@ -1166,9 +1173,17 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                                        : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi)));
                 const int64_t Mj = M + cur.dsum;
                 const int pj = cur.rend;
-                if (!ok) {  // this block the reference way (the last block padded with -0.0)
+                // a block without a prediction is added the reference way whatever
+                // S is, and so is the rest of its run (every block of [pos, rend)
+                // has none): the whole streak in one loop, the next block's values
+                // requested while this one's are added (a sum crossing zero or
+                // sitting on a binade edge makes such streaks: the slowest
+                // episodes' walks were 70-171 one-block fallbacks)
+                const bool streak = STREAK && !ok && cur.be == INT32_MIN;
+                const int pend = streak ? min(pj, nblk) : pos + 1;
+                if (!ok) {  // blocks [pos, pend) the reference way (the last block padded with -0.0)
 #ifdef SGMM_STAMPS
-                    ++n_slow;
+                    n_slow += pend - pos;
 #endif
                     const double2* vp = reinterpret_cast<const double2*>(sel + pos * kSumBlk);
                     double2 v[kSumBlk / 2];
@@ -1180,13 +1195,29 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                         s += v[j].x;
                         s += v[j].y;
                     }
+                    // the rest of a streak, 8 values per LDS round trip
+                    const double2* __restrict__ sp = vp + kSumBlk / 2;
+                    const double2* const se = vp + (pend - pos) * (kSumBlk / 2);
+                    for (; STREAK && sp < se; sp += 4) {
+                        const double2 a = sp[0], b = sp[1], c = sp[2], d = sp[3];
+                        s += a.x;
+                        s += a.y;
+                        s += b.x;
+                        s += b.y;
+                        s += c.x;
+                        s += c.y;
+                        s += d.x;
+                        s += d.y;
+                    }
                     S = s;
                     ib = binade_of(s, e, M);
                 }
                 // both successors' records were requested before the decision
+                // (a streak ends at the run's end: its record is rj)
+                const bool to_end = ok || streak;
                 M = ok ? Mj : M;
-                pos = ok ? pj : pos + 1;
-                cur = ok ? rj : rn;
+                pos = ok ? pj : pend;
+                cur = to_end ? rj : rn;
                 if (pos >= nblk) break;
             }
             L.S = ib ? from_binade(M, e) : S;
@@ -2011,7 +2042,7 @@ __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __re
         const int m = (int)min((int64_t)kScanWin, n - w0);
         for (int i = threadIdx.x; i < m; i += kScanThreads) sel[i] = x[w0 + i];
         __syncthreads();
-        S = exact_sum_window<kScanThreads>(sel, m, S, L);
+        S = exact_sum_window<kScanThreads, true>(sel, m, S, L);  // the adversary scan's instantiation
     }
     if (threadIdx.x == 0) *out = S;
 }
@@ -2135,7 +2166,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         __syncthreads();
         SGMM_STAMP(e, 12);
         for (int k = 0; k < segn; k += 4 * NT)  // windows of 4 values per thread
-            total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L);
+            total = exact_sum_window<NT, true>(sel + k, min(4 * NT, segn - k), total, L);
     }
     int w = my_trades;
 #pragma unroll

@@ -340,7 +340,13 @@ def _sum_cases():
             ("zero_runs", 0.0, np.concatenate([np.zeros(2000), env_like[:500], -np.zeros(3000), env_like[:33],
                                                np.zeros(17), [1e-300], np.zeros(1000)])),
             ("zero_runs_inf", 0.0, np.concatenate([np.zeros(500), [np.inf], np.zeros(600), [1.0]])),
-            ("zero_runs_init", 123.25, np.concatenate([np.zeros(1100), env_like[:300], np.zeros(5000)]))]
+            ("zero_runs_init", 123.25, np.concatenate([np.zeros(1100), env_like[:300], np.zeros(5000)])),
+            # streaks of blocks without a prediction (the walk adds a whole streak in one loop):
+            # a mean-zero walk crossing zero, sums cancelling to tiny values, streaks cut by runs
+            ("zero_mean_walk", 0.0, rng.normal(0, 1e-3, 20000)),
+            ("crossings", 0.0, np.tile([1.0, -1.0 + 2.0 ** -40, 2.0 ** -60, -(2.0 ** -61)], 2500)),
+            ("streaks_and_runs", 0.0, np.concatenate([np.tile([1e-3, -1e-3], 700), rng.normal(1e-3, 1e-4, 900),
+                                                      np.tile([5e-4, -5e-4 - 1e-18], 1100), rng.normal(2e-3, 1e-4, 3000)]))]
 
 
 @pytest.mark.parametrize("name,init,x", _sum_cases(), ids=[c[0] for c in _sum_cases()])
