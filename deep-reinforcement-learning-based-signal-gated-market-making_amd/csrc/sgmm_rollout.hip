@@ -1154,6 +1154,11 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
         // additions.  Both possible next records (pos + 1 and the run end) are
         // requested as soon as the current one arrives.
         constexpr int NB = NT / 4;
+        // the walk is the episode's serial chain: first call on its SIMD's issue
+        // while it runs (the other waves there are in their window phases)
+#ifndef SGMM_NO_WALK_PRIO
+        __builtin_amdgcn_s_setprio(3);
+#endif
         if (lane == 0 && nblk > 0) {
             int pos = 0;
             int e = 0;
@@ -1226,6 +1231,9 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
         if (threadIdx.x == 0 && blockIdx.x < 4096) { g_stamps[blockIdx.x][13] += n_iter; g_stamps[blockIdx.x][14] += n_slow; }
 #endif
         if (lane == 0 && nblk == 0) L.S = S;
+#ifndef SGMM_NO_WALK_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
     }
     __syncthreads();
     SGMM_STAMP(blockIdx.x, 10);
