@@ -1222,7 +1222,13 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                 const bool to_end = ok || streak;
                 M = ok ? Mj : M;
                 pos = ok ? pj : pend;
-                cur = to_end ? rj : rn;
+                // field by field: a whole-struct select was lowered to a scratch
+                // round trip per step
+                cur.mn = to_end ? rj.mn : rn.mn;
+                cur.mx = to_end ? rj.mx : rn.mx;
+                cur.dsum = to_end ? rj.dsum : rn.dsum;
+                cur.be = to_end ? rj.be : rn.be;
+                cur.rend = to_end ? rj.rend : rn.rend;
                 if (pos >= nblk) break;
             }
             L.S = ib ? from_binade(M, e) : S;
