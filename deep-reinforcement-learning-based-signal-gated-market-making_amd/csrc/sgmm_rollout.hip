@@ -990,14 +990,9 @@ struct SumLds {
 // and a barrier has passed; returns S + sel[0] + ... + sel[n-1] in sequential
 // float64 order in every thread.  S must be the same in every thread.  Ends
 // with a barrier (sel may then be refilled).
-// STREAK: a block without a prediction takes the rest of its run with it (one
-// loop of reference additions, no walk step per block).  It shortens the
-// walks of the episodes with long fallback streaks -- the slowest ones -- and
-// costs the others a little: on for the one-wave and the adversary scans
-// (config 3 scan 129 -> 115 us, config 4 53.3 -> 51.6 us), off for the
-// 512/1024-thread scans of small batches (config 2 scan 17.8 -> 19.3 us with
-// it; profiles/r04_ab/r04u*).
-template <int NT, bool STREAK = (NT == 4 * kWave)>
+// A block without a prediction takes the rest of its run with it: one loop of
+// reference additions, no walk step per block (see the walk below).
+template <int NT>
 __device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L) {
     static_assert(NT % (4 * kWave) == 0, "whole block waves");
     constexpr int NB = NT / 4;         // 16-value blocks per window
@@ -1180,11 +1175,11 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                 const int pj = cur.rend;
                 // a block without a prediction is added the reference way whatever
                 // S is, and so is the rest of its run (every block of [pos, rend)
-                // has none): the whole streak in one loop, the next block's values
-                // requested while this one's are added (a sum crossing zero or
-                // sitting on a binade edge makes such streaks: the slowest
-                // episodes' walks were 70-171 one-block fallbacks)
-                const bool streak = STREAK && !ok && cur.be == INT32_MIN;
+                // has none): the whole streak in one loop of 8 values per LDS
+                // round trip (a sum crossing zero or sitting on a binade edge makes
+                // such streaks: the slowest episodes' walks were 70-171 one-block
+                // fallbacks)
+                const bool streak = !ok && cur.be == INT32_MIN;
                 const int pend = streak ? min(pj, nblk) : pos + 1;
                 if (!ok) {  // blocks [pos, pend) the reference way (the last block padded with -0.0)
 #ifdef SGMM_STAMPS
@@ -1203,7 +1198,7 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                     // the rest of a streak, 8 values per LDS round trip
                     const double2* __restrict__ sp = vp + kSumBlk / 2;
                     const double2* const se = vp + (pend - pos) * (kSumBlk / 2);
-                    for (; STREAK && sp < se; sp += 4) {
+                    for (; sp < se; sp += 4) {
                         const double2 a = sp[0], b = sp[1], c = sp[2], d = sp[3];
                         s += a.x;
                         s += a.y;
@@ -2056,7 +2051,7 @@ __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __re
         const int m = (int)min((int64_t)kScanWin, n - w0);
         for (int i = threadIdx.x; i < m; i += kScanThreads) sel[i] = x[w0 + i];
         __syncthreads();
-        S = exact_sum_window<kScanThreads, true>(sel, m, S, L);  // the adversary scan's instantiation
+        S = exact_sum_window<kScanThreads>(sel, m, S, L);
     }
     if (threadIdx.x == 0) *out = S;
 }
@@ -2180,7 +2175,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         __syncthreads();
         SGMM_STAMP(e, 12);
         for (int k = 0; k < segn; k += 4 * NT)  // windows of 4 values per thread
-            total = exact_sum_window<NT, true>(sel + k, min(4 * NT, segn - k), total, L);
+            total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L);
     }
     int w = my_trades;
 #pragma unroll
