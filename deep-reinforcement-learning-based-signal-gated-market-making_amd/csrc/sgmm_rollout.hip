@@ -2059,25 +2059,27 @@ __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __re
 
 // ------------------------------------------------------------------ path scan (adversary)
 // 4 nsi-state machine (inventory x previous fill flags).  Per episode, one
-// NT-thread workgroup, segment by segment (kSeg ticks = 64 chunks of 64), the
+// NT-thread workgroup, segment by segment (kSeg ticks = 128 pieces of 32), the
 // state entering a segment carried over -- no bound on the episode length:
 //   1. the segment's fill codes -> LDS (coalesced);
-//   2. every (chunk, start state) pair walks its chunk over the LDS codes (8
-//      per round trip): the chunk's transducer, end state and trade count per
-//      start state (all NT threads: ~1 round of 64 steps at config 4, where
-//      one serial walker per table wave cost the table ~25 us);
-//   3. the end maps chained by pointer jumping (log2(64) rounds over all
-//      (chunk, state) pairs) -> each chunk's start state; trades = the sum of
-//      every chunk's count from its start state;
-//   4. one thread per chunk walks its 64 ticks from the start state and
+//   2. every (piece, start state) pair walks its piece over the LDS codes (8
+//      per round trip): the piece's transducer, end state and trade count per
+//      start state (all NT threads: 3 rounds of 32 steps at config 4, where
+//      one serial walker per table wave cost the table ~25 us; 64-tick pieces
+//      took 2 rounds of 64 steps, and twice as long in step 4);
+//   3. the end maps chained by pointer jumping (log2(128) rounds over all
+//      (piece, state) pairs) -> each piece's start state; trades = the sum of
+//      every piece's count from its start state;
+//   4. one thread per piece walks its 32 ticks from the start state and
 //      records the state of every tick;
 //   5. every thread gathers its ticks' rewards from the per-state planes
 //      rew[state * rs + row] (independent loads: one latency per segment;
 //      consecutive ticks in one state are consecutive addresses);
 //   6. the exact sequential float64 sum (exact_sum_window).
-// Dynamic LDS: [kSeg u64 codes / f64 rewards][kSeg states][2][64][ns] maps
-// [64][ns] trade counts [64] starts.
-constexpr int kSegChunks = kSeg / kChunk;
+// Dynamic LDS: [kSeg u64 codes / f64 rewards][kSeg states][2][128][ns] maps
+// [128][ns] trade counts [128] starts.
+constexpr int kArlSub = 32;                 // ticks per transducer piece (half a table chunk)
+constexpr int kSegChunks = kSeg / kArlSub;  // pieces per segment
 static size_t arl_scan_lds(int ns) { return (size_t)kSeg * 9 + (size_t)3 * kSegChunks * ns + kSegChunks; }
 template <int NT>
 __global__ __launch_bounds__(NT) void k_path_scan_arl(
@@ -2106,7 +2108,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
     double total = 0.0;
     for (int seg0 = 0; seg0 < T; seg0 += kSeg) {
         const int segn = min(kSeg, T - seg0);
-        const int segch = (segn + kChunk - 1) / kChunk;
+        const int segch = (segn + kArlSub - 1) / kArlSub;
         for (int i = tid; i < segn; i += NT) fl[i] = F[seg0 + i];
         __syncthreads();
         SGMM_STAMP(e, 1);
@@ -2114,7 +2116,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         for (int i = tid; i < segch * ns; i += NT) {
             const int k = i / ns;
             int st = i - k * ns, cnt = 0;
-            const int ta = k * kChunk, tb = min(segn, ta + kChunk);
+            const int ta = k * kArlSub, tb = min(segn, ta + kArlSub);
             for (int t8 = ta; t8 < tb; t8 += 8) {
                 uint64_t f[8];
 #pragma unroll
@@ -2156,7 +2158,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         carry = pre[(segch - 1) * ns + carry];
         if (tid < segch) {  // chunk tid's state path
             int st = start[tid];
-            const int ta = tid * kChunk, tb = min(segn, ta + kChunk);
+            const int ta = tid * kArlSub, tb = min(segn, ta + kArlSub);
             for (int t8 = ta; t8 < tb; t8 += 8) {
                 uint64_t f[8];
 #pragma unroll
