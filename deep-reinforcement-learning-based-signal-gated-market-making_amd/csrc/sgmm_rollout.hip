@@ -1741,6 +1741,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
         fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
 #ifndef SGMM_NO_FR_PRIO
         if ((tt & 7) == 7) {
+            // (graded levels 0-3 at 0.3 / 0.6 / 1.25 extra slots per tick measured
+            // the same: 664-665 vs 664-668 us per config-3 generation, r04ab_*)
             if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
         }
