@@ -918,6 +918,7 @@ constexpr int kScanAt512 = 512;   // 512 up to this many, one wave above
 constexpr int kScanArlAt1024 = 1024;  // adversary path scan: 1024 threads up to this many, kScanBlock above
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int32_t kZeroRun = INT32_MAX;  // a block's prediction: all its values are +-0.0
+constexpr int kHeadBlocks = 8;           // blocks added the reference way when a sum starts at +0.0
 constexpr int64_t kEdge = 1LL << 40;  // prediction margin at the binade edges (2^-12 relative)
 static_assert(kChunk % kSumTpt == 0, "a thread's ticks lie in one chunk");
 
@@ -1083,6 +1084,36 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
         const int rq = later ? __ffsll((unsigned long long)later) - 1 : kWave;
         // segmented suffix min / max of the in-wave prefix extremes over [lane, rq)
         int64_t amn = zl + mn, amx = zl + mx;
+#ifndef SGMM_SUFFIX_BPERMUTE
+        // inside each 16-lane row by DPP row shifts (lane i reads lane i + d of its
+        // row: no LDS round trip), then across rows from the three row heads
+        // (readlane): a lane whose run goes on into row k > its row takes row k's
+        // head, which covers [16k, min(rq, 16k + 16)) of the same run
+        {
+            const int rl_ = lane & 15;
+#define SGMM_SEG_STEP(D)                                                                   \
+    {                                                                                      \
+        const int64_t omn = (int64_t)dpp64<0x100 + D>((uint64_t)INT64_MAX, (uint64_t)amn); \
+        const int64_t omx = (int64_t)dpp64<0x100 + D>((uint64_t)INT64_MIN, (uint64_t)amx); \
+        if (rl_ + D < 16 && lane + D < rq) {                                               \
+            amn = min(amn, omn);                                                           \
+            amx = max(amx, omx);                                                           \
+        }                                                                                  \
+    }
+            SGMM_SEG_STEP(1) SGMM_SEG_STEP(2) SGMM_SEG_STEP(4) SGMM_SEG_STEP(8)
+#undef SGMM_SEG_STEP
+            const int row = lane >> 4;
+#pragma unroll
+            for (int k = 1; k < 4; ++k) {
+                const int64_t hmn = (int64_t)readlane64((uint64_t)amn, 16 * k);
+                const int64_t hmx = (int64_t)readlane64((uint64_t)amx, 16 * k);
+                if (row < k && rq > 16 * k) {
+                    amn = min(amn, hmn);
+                    amx = max(amx, hmx);
+                }
+            }
+        }
+#else
 #pragma unroll
         for (int d = 1; d < kWave; d <<= 1) {
             const int64_t omn = shfl_i64(amn, min(lane + d, kWave - 1));
@@ -1092,6 +1123,7 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                 amx = max(amx, omx);
             }
         }
+#endif
         const int64_t zr = shfl_i64(zl, min(rq, kWave - 1));
         SumRec rc;
         rc.mn = amn - zl;
@@ -1159,8 +1191,35 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
             int e = 0;
             int64_t M = 0;
             bool ib = binade_of(S, e, M);  // S = M * 2^(e-52) exactly while ib
-            SumRec cur = L.rec[0];
-            while (true) {
+#ifndef SGMM_NO_HEAD_STREAK
+            // an episode's sum starts at +0.0 and doubles every few ticks at first
+            // (ticks 2, 3, 6, 16, 22, 43, 85, ...): its first kHeadBlocks blocks
+            // are walk steps that almost all fall back, so they are added the
+            // reference way in one loop
+            if (__double_as_longlong(S) == 0) {
+                const int pe = min(kHeadBlocks, nblk);
+                const double2* hp = reinterpret_cast<const double2*>(sel);
+                double s = S;
+                for (int b = 0; b < pe; ++b) {
+                    double2 v[kSumBlk / 2];
+#pragma unroll
+                    for (int j = 0; j < kSumBlk / 2; ++j) v[j] = hp[b * (kSumBlk / 2) + j];
+#pragma unroll
+                    for (int j = 0; j < kSumBlk / 2; ++j) {
+                        s += v[j].x;
+                        s += v[j].y;
+                    }
+                }
+#ifdef SGMM_STAMPS
+                n_slow += pe;
+#endif
+                S = s;
+                ib = binade_of(s, e, M);
+                pos = pe;
+            }
+#endif
+            SumRec cur = L.rec[min(pos, NB - 1)];
+            while (pos < nblk) {
 #ifdef SGMM_STAMPS
                 ++n_iter;
 #endif
