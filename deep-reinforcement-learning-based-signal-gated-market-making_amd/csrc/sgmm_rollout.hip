@@ -1226,10 +1226,14 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
                 const SumRec rn = L.rec[min(pos + 1, NB - 1)];
                 const SumRec rj = L.rec[min(cur.rend, NB - 1)];
                 // (a zero run is skipped unless S is -0.0: only the API's init can make it so)
-                const bool ok = (cur.be == kZeroRun && (ib || __double_as_longlong(S) != INT64_MIN)) ||
-                                (ib && cur.be == e &&
-                                (M > 0 ? (M + cur.mn >= kMLo && M + cur.mx <= kMHi)
-                                       : (M + cur.mx <= -kMLo && M + cur.mn >= -kMHi)));
+                // every term evaluated, combined bitwise: no branch per term on the
+                // walk's serial chain (the short-circuit form compiled to 4-5 branches;
+                // measured the same, profiles/r04_ab/r04af*)
+                const int64_t lo_ = M + cur.mn, hi_ = M + cur.mx;
+                const bool pos_ok = (lo_ >= kMLo) & (hi_ <= kMHi);
+                const bool neg_ok = (hi_ <= -kMLo) & (lo_ >= -kMHi);
+                const bool zero_ok = (cur.be == kZeroRun) & (ib | (__double_as_longlong(S) != INT64_MIN));
+                const bool ok = zero_ok | (ib & (cur.be == e) & (M > 0 ? pos_ok : neg_ok));
                 const int64_t Mj = M + cur.dsum;
                 const int pj = cur.rend;
                 // a block without a prediction is added the reference way whatever
