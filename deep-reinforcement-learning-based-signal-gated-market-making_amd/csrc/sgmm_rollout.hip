@@ -178,6 +178,15 @@ __device__ __forceinline__ int next_state_arl(int s, int code) {
     const int fb = code & 1, fs = code >> 1;
     return (((s >> 2) + fb - fs) << 2) | (fs << 1) | fb;
 }
+// one tick of the walk from state s over the tick's 2-bit fill codes f (state x
+// at bits 2x): next_state_arl with the inventory step as a byte lookup
+// (code 0, 1, 2, 3 -> 0, +4, -4, 0 on s & ~3) and the trade count
+__device__ __forceinline__ int arl_step(int s, uint64_t f, int& cnt) {
+    const int c = (int)(f >> (2 * s)) & 3;
+    cnt += c != 0;
+    const int d = __builtin_amdgcn_sbfe(0x00FC0400, 8 * c, 8);
+    return ((s + d) & ~3) | c;
+}
 
 // ------------------------------------------------------------------ table
 // Block = 64 consecutive ticks of one episode x nsi inventory states: wave w
@@ -2182,6 +2191,16 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
             const int k = i / ns;
             int st = i - k * ns, cnt = 0;
             const int ta = k * kArlSub, tb = min(segn, ta + kArlSub);
+            if (tb - ta == kArlSub) {  // a whole piece: no per-tick bound check
+#pragma unroll 1
+                for (int t8 = ta; t8 < tb; t8 += 8) {
+                    uint64_t f[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) f[j] = fl[t8 + j];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) st = arl_step(st, f[j], cnt);
+                }
+            } else
             for (int t8 = ta; t8 < tb; t8 += 8) {
                 uint64_t f[8];
 #pragma unroll
@@ -2221,9 +2240,23 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         __syncthreads();
         SGMM_STAMP(e, 7);
         carry = pre[(segch - 1) * ns + carry];
-        if (tid < segch) {  // chunk tid's state path
+        if (tid < segch) {  // piece tid's state path
             int st = start[tid];
             const int ta = tid * kArlSub, tb = min(segn, ta + kArlSub);
+            if (tb - ta == kArlSub) {  // a whole piece: no per-tick bound check
+                int unused = 0;
+#pragma unroll 1
+                for (int t8 = ta; t8 < tb; t8 += 8) {
+                    uint64_t f[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) f[j] = fl[t8 + j];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        stt[t8 + j] = (uint8_t)st;
+                        st = arl_step(st, f[j], unused);
+                    }
+                }
+            } else
             for (int t8 = ta; t8 < tb; t8 += 8) {
                 uint64_t f[8];
 #pragma unroll
