@@ -1,0 +1,198 @@
+// sgmm_rollout.h -- device layout and helpers shared by the rollout translation
+// units (sgmm_rollout.hip: tables, path scans, host entry points;
+// sgmm_frontier.hip: the frontier kernel).
+#pragma once
+
+#include "sgmm_device.h"
+#include "sgmm_ga_device.h"
+#include "sgmm_internal.h"
+
+namespace sgmm {
+
+constexpr int kChunk = 64;          // ticks per chunk in the path scan
+constexpr int kSeg = 4096;          // ticks summed per LDS segment
+constexpr int kScanBlock = 256;
+constexpr int kMaxLen = 1 << 17;    // max ticks per episode of the no-adversary table path (its scan's LDS chunk tables)
+
+struct EpArrays {
+    const int32_t* genome;
+    const int32_t* adv;
+    const int64_t* tick_off;
+    const int32_t* len;
+    const int64_t* step_off;
+    const int32_t* param;
+    int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
+    const int32_t* order;  // frontier kernel: episode of order position p (NULL: p)
+    // frontier kernel: every episode of the launch is cut into ngrp groups of
+    // 64 chunks, one wave each (chunks of frontier_len(T, ngrp) ticks); the
+    // path scan derives the same chunk layout from it
+    int32_t ngrp;
+};
+
+// Where an episode's genomes come from: materialized rows (pop != nullptr) or
+// the current generation's ask() of the GA state, generated in the kernel
+// (never written to memory): individual i0 + genome[e], values identical to
+// what sgmm_ga_ask writes.  With several populations (pop_eps > 0) episode e
+// belongs to population k = e / pop_eps, whose state, masters and Philox key
+// sit at st + k, master_* + k * *_pstride and seeds[k].
+struct GenomeSrc {
+    const float* mm;
+    int64_t mm_stride;
+    const float* adv;
+    int64_t adv_stride;
+    const sgmm_ga_state* st;
+    const float* master_mm;
+    const float* master_adv;
+    uint64_t seed;            // population 0's key when seeds == nullptr
+    int32_t i0;
+    int32_t pop_eps;          // episodes per population (0: one population)
+    const uint64_t* seeds;    // [K] per-population keys, or nullptr
+    int64_t mm_pstride, adv_pstride;
+};
+
+constexpr int kAdvParams = 74;  // AdversaryPolicy weights = first 74 floats of the genome
+constexpr int kAdvGenome = 1250;  // adversary evolver masters are TradingPolicy() genomes (model.py:63)
+
+// Stage the policy genome (n floats) of individual gi of episode e's
+// population and, when ga != nullptr and ai >= 0, the adversary weights of
+// individual ai into LDS.  Every thread of the block calls; the caller
+// synchronizes.
+__device__ inline void stage_genomes(const GenomeSrc& src, int e, int gi, int ai, int n, float* gs, float* ga) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (src.st) {
+        const int k = src.pop_eps > 0 ? e / src.pop_eps : 0;
+        const sgmm_ga_state* st = src.st + k;
+        const uint64_t seed = src.seeds ? src.seeds[k] : src.seed;
+        const float* master = src.master_mm + (int64_t)k * src.mm_pstride;
+        const uint32_t gen = (uint32_t)st->gen;
+        const float sig = (float)st->sigma_mm;
+        for (int k4 = tid; k4 < (n + 3) / 4; k4 += nt) {
+            float v[4];
+            ask_row4(master, n, sig, seed, 0u, gen, (uint32_t)(src.i0 + gi), k4, v);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * k4 + q < n) gs[4 * k4 + q] = v[q];
+        }
+        if (ga && ai >= 0) {
+            const float siga = (float)st->sigma_adv;
+            const float* amaster = src.master_adv + (int64_t)k * src.adv_pstride;
+            for (int k4 = tid; k4 < (kAdvParams + 3) / 4; k4 += nt) {
+                float v[4];
+                ask_row4(amaster, kAdvParams, siga, seed, 1u, gen, (uint32_t)(src.i0 + ai), k4, v);
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (4 * k4 + q < kAdvParams) ga[4 * k4 + q] = v[q];
+            }
+        }
+    } else {
+        const float* __restrict__ row = src.mm + (int64_t)gi * src.mm_stride;
+        for (int k = tid; k < n; k += nt) gs[k] = row[k];
+        if (ga && ai >= 0) {
+            const float* __restrict__ arow = src.adv + (int64_t)ai * src.adv_stride;
+            for (int k = tid; k < kAdvParams; k += nt) ga[k] = arow[k];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ transition maps
+// A step's effect on the (<= 8) inventory states is a map state -> state,
+// one byte per state in a u64 (byte x = image of state x).  Composition is
+// two v_perm_b32 (byte x of the result = byte a[x] of b), so a wave of 64
+// ticks builds the inclusive prefix of its chunk with six DPP steps and the
+// path of any start state is one byte lookup.
+constexpr uint64_t kIdentityMap = 0x0706050403020100ull;  // x -> x for x = 0..7
+
+__device__ __forceinline__ uint32_t map_get(uint64_t m, uint32_t x) {
+    return (uint32_t)(m >> (8u * x)) & 0xFFu;
+}
+
+// "first a, then b": (a ; b)[x] = b[a[x]]
+__device__ __forceinline__ uint64_t map_then(uint64_t a, uint64_t b) {
+    const uint32_t bl = (uint32_t)b, bh = (uint32_t)(b >> 32);
+    const uint32_t lo = __builtin_amdgcn_perm(bh, bl, (uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_perm(bh, bl, (uint32_t)(a >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// inclusive prefix composition over the wave (row shifts, then row
+// broadcasts; a lane without a source composes the identity)
+__device__ __forceinline__ uint64_t wave_map_scan(uint64_t m) {
+#define SGMM_MSTEP(CTRL, RM) m = map_then(dpp64<CTRL, RM>(kIdentityMap, m), m);
+    SGMM_MSTEP(0x111, 0xF) SGMM_MSTEP(0x112, 0xF) SGMM_MSTEP(0x114, 0xF)
+    SGMM_MSTEP(0x118, 0xF) SGMM_MSTEP(0x142, 0xA) SGMM_MSTEP(0x143, 0xC)
+#undef SGMM_MSTEP
+    return m;
+}
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, kWave);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, kWave);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint32_t chunk_base(int64_t step_off, int e) {
+    // chunk-map slot of episode e: regions of ceil(len/64) never overlap
+    return (uint32_t)((step_off + (int64_t)kChunk * e) / kChunk);
+}
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <int N>
+struct IntC {
+    static constexpr int value = N;
+};
+// number of lanes below this one whose bit is set in m
+__device__ __forceinline__ int mbcnt64(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
+constexpr int kFrPrioExtra = 160;      // a walk's issue priority from 0.625 extra slots per tick on average
+constexpr int kFrontierMaxWaves = 4;   // waves (64-chunk groups) per episode
+constexpr int kFrontierRecs = kFrontierLanes * kFrontierMaxWaves;  // chunk records per episode: e * 256 + c
+constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
+typedef __attribute__((address_space(3))) const float lds_cf;
+typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
+// ticks per chunk with nw waves (64 nw chunks) per episode
+__host__ __device__ __forceinline__ int frontier_len(int T, int nw) {
+    const int c = (T + kFrontierLanes * nw - 1) / (kFrontierLanes * nw);
+    return c < 4 ? 4 : (c + 3) & ~3;  // a multiple of 4: a scan thread's 4 ticks stay in one chunk
+}
+// the episode's block of plane rows: nw groups of frontier_len(T, nw) x 64 rows
+// <= T + 256 nw rows (T rounded up to 64 nw chunks of a multiple of 4),
+// starting on a 128-byte line (16 rows), so blocks at step_off + 1040 e
+// (rounded up to 16) never overlap and no two episodes share a line; the plane
+// stride covers total_steps + 1040 n (rew_stride).  Group g's rows start at
+// base + g * CL * 64 (frontier_row within the group)
+constexpr int kFrontierPad = 4 * kFrontierRecs + 16;  // plane rows per episode beyond its ticks
+__device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
+    return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
+}
+// Within a group's block, the reward of chunk (lane) l at tick offset u: rows
+// of the 64 chunks at one tick offset (u * 64 + l) -- a walk's store of one
+// tick is one 512-byte row per plane, four whole 128-byte lines.  (Round 3's
+// 4-tick groups, ((u >> 2) * 64 + l) * 4 + (u & 3), gave the scan one line per 4
+// ticks but left lines part-written across ticks: 254 vs 155 MB written per
+// config-3 launch, profiles/r03_pmc_traffic_c3.json vs r04_pmc_traffic_c3.json.)
+__host__ __device__ __forceinline__ int64_t frontier_row(int u, int l) {
+    return (int64_t)u * kFrontierLanes + l;
+}
+
+// ------------------------------------------------------------------ frontier kernel launch
+struct FrontierArgs {
+    sgmm_ticks tk;
+    EpArrays ep;
+    const sgmm_env_params* params;
+    GenomeSrc src;
+    int32_t inv_min, nsi;
+    uint64_t* cmaps;
+    uint32_t* ctr32;
+    uint32_t* kinfo;
+    double* rew;
+};
+
+// launches the frontier kernel for hidden = 16 / 32 and nsi inventory states
+// (sgmm_frontier.hip): grid = episodes x ep.ngrp waves
+int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, hipStream_t s, const FrontierArgs& fa);
+
+}  // namespace sgmm

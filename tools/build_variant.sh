@@ -2,6 +2,6 @@
 # usage: bash tools/build_variant.sh NAME -DFLAG[=V] ...   (run it with SGMM_LIB=tools/variants/libsgmm_NAME.so)
 set -e
 name=$1; shift
-D=deep-reinforcement-learning-based-signal-gated-market-making_amd/csrc
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -shared -ffp-contract=off --offload-arch=gfx950 "$@" \
-  -o tools/variants/libsgmm_$name.so $D/sgmm_capi.hip $D/sgmm_rollout.hip $D/sgmm_ga.hip $D/sgmm_bundle.hip $D/sgmm_sgu2.hip
+mkdir -p tools/variants
+python deep-reinforcement-learning-based-signal-gated-market-making_amd/build.py \
+  --out tools/variants/libsgmm_$name.so -- "$@"

@@ -32,11 +32,11 @@ eb = sg.EpisodeBatch(np.arange(n), [ticks.segments[s0][0]] * n, [4560] * n, np.z
 eng = sg.RolloutEngine(dev)
 if MODE == "slots":
     L = _lib.load()
-    L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     eng.fitness(ticks, eb, params, pop, H)
     torch.cuda.synchronize()
     h = np.zeros((n, 8), np.uint64)
-    L.sgmm_debug_tstamps(h.ctypes.data, n)
+    L.sgmm_debug_frontier_tstamps(h.ctypes.data, n)
     np.save("/tmp/frontier_slots.npy", h[:, 2].astype(np.int64))
     print("slots p50/p90/p99/max", np.percentile(h[:, 2], [50, 90, 99]).tolist(), int(h[:, 2].max()))
     sys.exit(0)

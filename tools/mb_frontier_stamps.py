@@ -17,7 +17,7 @@ import sgmm_pkg
 sg = sgmm_pkg.load()
 from sgmm_amd import _lib, synthetic
 L = _lib.load()
-L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
 H = int(os.environ.get("H", 32))
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 sigma = float(sys.argv[2]) if len(sys.argv) > 2 else 0.05
@@ -38,7 +38,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 n = P + NV
 h = np.zeros((n, 8), np.uint64)
-L.sgmm_debug_tstamps(h.ctypes.data, n)
+L.sgmm_debug_frontier_tstamps(h.ctypes.data, n)
 h = h.astype(np.float64)
 for name, sl, T in (("train", slice(0, P), 4560), ("val", slice(P, P + NV), 912))[:2 if NV else 1]:
     x = h[sl]

@@ -16,8 +16,8 @@ import sgmm_pkg
 sg = sgmm_pkg.load()
 from sgmm_amd import _lib, synthetic
 L = _lib.load()
-L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-L.sgmm_debug_thwid.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_frontier_thwid.argtypes = [ctypes.c_void_p, ctypes.c_int]
 H, K = 32, 5
 P = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 dev = torch.device("cuda")
@@ -40,9 +40,9 @@ for _ in range(3):
     eng.fitness(ticks, eb, params, pop, H)
 torch.cuda.synchronize()
 h = np.zeros((n, 8), np.uint64)
-L.sgmm_debug_tstamps(h.ctypes.data, n)
+L.sgmm_debug_frontier_tstamps(h.ctypes.data, n)
 hw = np.zeros((n, 2), np.uint32)
-L.sgmm_debug_thwid(hw.ctypes.data, n)
+L.sgmm_debug_frontier_thwid(hw.ctypes.data, n)
 t0 = h[:, 0].astype(np.int64); t1 = h[:, 1].astype(np.int64)
 base = t0.min()
 s, e_ = (t0 - base) * 10, (t1 - base) * 10  # ns

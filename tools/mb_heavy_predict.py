@@ -19,8 +19,8 @@ sg = sgmm_pkg.load()
 from sgmm_amd import _lib, synthetic
 from sgmm_amd._lib import ptr, stream_ptr
 L = _lib.load()
-L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-L.sgmm_debug_thwid.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+L.sgmm_debug_frontier_thwid.argtypes = [ctypes.c_void_p, ctypes.c_int]
 sys.path.insert(0, str(ROOT))
 import bench
 H, K, P, T, Tv = 32, 5, 512, 4560, 912
@@ -57,14 +57,14 @@ for g in gens:
     torch.cuda.synchronize()
     del os.environ["SGMM_TABLE_PATH"]
     n = K * P
-    L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    hh = np.zeros((32768, 8), np.uint64); L.sgmm_debug_tstamps(hh.ctypes.data, 32768)
-    hwh = np.zeros((32768, 2), np.uint32); L.sgmm_debug_thwid(hwh.ctypes.data, 32768)
+    L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    hh = np.zeros((32768, 8), np.uint64); L.sgmm_debug_frontier_tstamps(hh.ctypes.data, 32768)
+    hwh = np.zeros((32768, 2), np.uint32); L.sgmm_debug_frontier_thwid(hwh.ctypes.data, 32768)
     split = hh[16384:16384 + n, 0] != 0  # second chunk groups of split episodes (SGMM_FRONTIER_NW=3)
     h = np.concatenate([hh[:n], hh[16384:16384 + n][split]])
     hw = np.concatenate([hwh[:n], hwh[16384:16384 + n][split]])
     hh[:] = 0
-    L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.sgmm_debug_frontier_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     tag = os.environ.get("TAG", "")
     np.savez(ROOT / f"gpurun_out/heavy{tag}_g{g}.npz", stamps=h, hwid=hw, nsplit=int(split.sum()),
              phis=np.array([p for p, _, _ in spec["pops"]]))
