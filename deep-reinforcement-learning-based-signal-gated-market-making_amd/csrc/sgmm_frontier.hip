@@ -4,6 +4,9 @@
 // population -- per tick the TradingPolicy forward (models/model.py:5-26) and
 // FTPEnv.step (Env/market_env.py:22-67) -- for the inventory states a chunk's
 // paths occupy; the path scan (sgmm_rollout.hip) sums the rewards.
+#include <cstdlib>
+#include <cstring>
+
 #include "sgmm_rollout.h"
 
 namespace sgmm {
@@ -44,7 +47,7 @@ __device__ unsigned int g_thwid[kStampWaves][2];  // HW_ID, XCC_ID of each wave
 // the launch with the path scans fused in measured no faster:
 // tools/experiments/round3_opt_in_paths.patch.)
 template <int H, int NSI>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier(FrontierArgs args) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier_r4(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16, KS = H / 4;
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int64_t rbase = frontier_base(so, e) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int64_t rbase = frontier_base(so, e, nw) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
     const int t0 = c * CL;
     const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
 
@@ -526,7 +529,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = (int64_t)e * kFrontierRecs + c;
+        const int64_t ci = frontier_rec(e, nw, c);
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
@@ -534,9 +537,421 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     }
 }
 
+// ------------------------------------------------------------------ frontier kernel (round 5)
+// The same walk, with each slot's MLP restructured for the SIMD's pipes
+// (tools/mb/mb_xwave3.hip: one wave's vector ops do not overlap its own MFMAs,
+// but another wave's float ops run beside them at full rate):
+//   - layer 1 on the matrix core: per 16-column tile q and neuron half hf one
+//     v_mfma_f32_16x16x4_f32 with A = W1 rows in the order that makes D's
+//     registers layer 2's B operand (D row 4g + r = neuron 16 hf + 4r + g, the
+//     B operand of k-step 4 hf + r), B = the column's inputs (s1, s2, inv/2, 0)
+//     read from a per-column LDS row, C = b1: the MFMA's k-ordered fused chain
+//     b1 + w0 s1 + w1 s2 + w2 x2 is the canonical one (the trailing + 0 * 0
+//     only turns -0 into +0, which relu maps to +0 either way) -- this replaces
+//     the 3 fmas per (neuron, column) of the vector layer 1;
+//   - layer 2 as one block of MFMAs (no vector work interleaved);
+//   - relu and the transpose through LDS one 16-neuron half at a time (5 KB
+//     instead of 9 KB), layer 3 as the two canonical output chains;
+//   - a lane whose paths have merged keeps one trade count and stores its
+//     slot-0 reward straight from the register.
+// <= 128 VGPRs and <= 10 KB of LDS (H = 32, 5 states): four walks per SIMD.
+template <int H, int NSI>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_policy_frontier(FrontierArgs args) {
+    static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16, KS = H / 4;
+    constexpr int HP = 20;  // LDS row pitch (floats) of one transposed 16-neuron half
+    constexpr int kHb = kWave * HP * 4;
+    // `big`: the staged genome, then the transpose rows (also the columns'
+    // layer-1 inputs)
+    constexpr int kBig = L::N * 4 > kHb ? L::N * 4 : kHb;
+    __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
+    __shared__ __attribute__((aligned(16))) float c1s[NT][4][4];   // layer-1 C: [hf][g][r] = b1[16 hf + 4r + g]
+    __shared__ __attribute__((aligned(16))) float b2s[H];
+    __shared__ __attribute__((aligned(8))) float sig[kWave][2];    // the tick's signals of each chunk
+    __shared__ double px[5][kWave];  // the tick's prices of each chunk (for the extra slots' FPT steps)
+    // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
+    // successor (bits 9-11) and the fill (bit 12) written back by the column
+    __shared__ uint16_t pl[kWave * (NSI - 1)];
+
+    const sgmm_ticks& tk = args.tk;
+    const EpArrays& ep = args.ep;
+    const sgmm_env_params* __restrict__ params = args.params;
+    const GenomeSrc& src = args.src;
+    const int32_t inv_min = args.inv_min, nsi = args.nsi;
+    uint64_t* __restrict__ cmaps = args.cmaps;
+    uint32_t* __restrict__ ctr32 = args.ctr32;
+    uint32_t* __restrict__ kinfo = args.kinfo;
+    double* __restrict__ rew = args.rew;
+    const int nw = ep.ngrp;
+    const int pos = (int)blockIdx.x / nw, cg = (int)blockIdx.x - pos * nw;
+    const int e = ep.order ? ep.order[pos] : pos;
+    const int32_t T = ep.len[e];
+    if (T <= 0) return;  // block-uniform
+    const int CL = frontier_len(T, nw);
+    const int nch = (T + CL - 1) / CL;
+    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
+    const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
+    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
+    const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
+    const int64_t rbase = frontier_base(so, e, nw) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int t0 = c * CL;
+    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
+
+    float* gsm = reinterpret_cast<float*>(big);
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __syncthreads();
+    if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
+    if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
+    if (lane < H) {
+        b2s[lane] = gsm[L::B2 + lane];
+        c1s[lane >> 4][lane & 3][(lane >> 2) & 3] = gsm[L::B1 + lane];  // neuron lane = 16 hf + 4 r + g
+    }
+    // A of layer 1, lane (g, col): W1[16 hf + 4 (col % 4) + col / 4][g], 0 at g = 3
+    float a1[NT];
+#pragma unroll
+    for (int hf = 0; hf < NT; ++hf)
+        a1[hf] = grp < 3 ? gsm[L::W1 + 3 * (16 * hf + 4 * (col & 3) + (col >> 2)) + grp] : 0.0f;
+    float w2f[NT][KS];  // A of layer 2: neuron 16 rt + col, k = 4 i + grp
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt)
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+    __syncthreads();  // gsm is dead from here
+    float* hb = reinterpret_cast<float*>(big);  // [64][HP]; rows [64][4]: the columns' inputs
+    const sgmm_env_params p = params[ep.param[e]];
+
+    // per-lane path bookkeeping: byte s of cur = the state of the path that
+    // started the chunk in state s (tracked starts: bits of sset)
+    const uint32_t all = (1u << nsi) - 1u;
+    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
+    uint64_t cur = kIdentityMap;
+    // trade count along the path from each tracked start until the paths
+    // merge (16 bits per start, two per word: a chunk has < 2^16 ticks), then
+    // one count for the merged path
+    uint32_t cnt[(NSI + 1) / 2];
+#pragma unroll
+    for (int s = 0; s < (NSI + 1) / 2; ++s) cnt[s] = 0;
+    uint32_t mcnt = 0;
+    bool merged = __builtin_popcount(sset) <= 1;
+    int kc = merged ? 0 : CL;  // merge offset (CL: never)
+    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
+#ifdef SGMM_STAMPS
+    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_s8 = 0, lite_s16 = 0;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
+#endif
+    int64_t ti = tick_of(0);
+    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
+    int fr_extra = 0;
+
+    // layers 1-3 for the columns of this slot (their inputs in the rows of
+    // hb as (s1, s2, inv/2, 0)); tiles >= NQ are skipped; o0 / o1 = the
+    // outputs of this lane's column
+    auto mlp = [&](auto nq, float& o0, float& o1, auto&& after_layer2) {
+        constexpr int NQ = decltype(nq)::value;
+        float xb[NQ];  // B of layer 1, lane (grp, col): input grp of column 16 q + col
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) xb[q] = hb[(16 * q + col) * 4 + grp];
+        f32x4 acc[NQ][NT];
+        // two column tiles at a time: their layer-1 MFMAs, relu, then their
+        // layer-2 MFMAs as one block (h1 of two tiles live, not four)
+#pragma unroll
+        for (int q0 = 0; q0 < NQ; q0 += 2) {
+            constexpr int Q2 = NQ < 2 ? NQ : 2;
+            f32x4 h1[Q2][NT];
+#pragma unroll
+            for (int hf = 0; hf < NT; ++hf) {
+                const f32x4 cc = *reinterpret_cast<const f32x4*>(&c1s[hf][grp][0]);
+#pragma unroll
+                for (int q = 0; q < Q2; ++q)
+                    h1[q][hf] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[hf], xb[q0 + q], cc, 0, 0, 0);
+            }
+#pragma unroll
+            for (int q = 0; q < Q2; ++q)
+#pragma unroll
+                for (int hf = 0; hf < NT; ++hf)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) h1[q][hf][r] = relu(h1[q][hf][r]);
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt) {
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(&b2s[16 * rt + 4 * grp]);
+#pragma unroll
+                for (int q = 0; q < Q2; ++q) acc[q0 + q][rt] = bb;
+            }
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
+#pragma unroll
+                for (int q = 0; q < Q2; ++q)
+#pragma unroll
+                    for (int rt = 0; rt < NT; ++rt)
+                        acc[q0 + q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[q][i >> 2][i & 3],
+                                                                              acc[q0 + q][rt], 0, 0, 0);
+        }
+        after_layer2();
+        asm volatile("" ::: "memory");  // the input rows are read before the transpose overwrites them
+        o0 = w3i[2 * H];
+        o1 = w3i[2 * H + 1];
+#pragma unroll
+        for (int rt = 0; rt < NT; ++rt) {
+            // relu'd neurons 16 rt + 4 grp + r of column 16 q + col -> row 16 q + col
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                f32x4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+                *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 4 * grp]) = v;
+            }
+            // layer 3 of this lane's column over neurons 16 rt .. 16 rt + 15, in
+            // order; the weight pairs are read where they are used (an opaque
+            // base: hoisted, the 64 floats would take 64 registers)
+#pragma unroll 1
+            for (int j4 = 0; j4 < 4; ++j4) {
+                lds_cf* w3p = (lds_cf*)(&w3i[2 * (16 * rt + 4 * j4)]);
+                asm volatile("" : "+v"(w3p));
+                const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+                for (int r2 = 0; r2 < 2; ++r2) {
+                    const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 4 * r2);
+                    o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                    o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                    o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                    o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                }
+            }
+            asm volatile("" ::: "memory");  // this half's rows are read before the next half is written
+        }
+    };
+
+#pragma unroll 1
+    for (int tt = 0; tt < CL; ++tt) {
+        const bool act = tt < ntl;
+        const float s1 = ns1, s2 = ns2;
+        const int64_t tcur = ti;
+        ti = tick_of(tt + 1);
+        ns1 = tk.s1n[ti];
+        ns2 = tk.s2n[ti];
+        // frontier: the distinct current states of the tracked paths
+        uint32_t fmask = 0;
+        if (merged) {
+            fmask = 1u << map_get(cur, p0);
+        } else {
+#pragma unroll
+            for (int s = 0; s < NSI; ++s)
+                if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
+        }
+        if (!act) fmask = 0;
+        // Slot 0: each lane's first frontier state in its own column (most
+        // ticks need nothing more).  Slots 1..: the remaining (chunk, state)
+        // pairs packed densely into the 64 columns, each with its own inputs.
+        const uint32_t ext = fmask & (fmask - 1u);  // frontier states after the first
+        int epfx = 0, etot = 0;
+        if (__ballot(ext != 0u)) {
+            *reinterpret_cast<f32x2*>(&sig[lane][0]) = f32x2{s1, s2};
+            const uint32_t nex = (uint32_t)__builtin_popcount(ext);
+            const uint64_t eb0 = __ballot(nex & 1u), eb1 = __ballot(nex & 2u), eb2 = __ballot(nex & 4u);
+            epfx = mbcnt64(eb0) + 2 * mbcnt64(eb1) + 4 * mbcnt64(eb2);  // first pair of this lane
+            etot = __popcll(eb0) + 2 * __popcll(eb1) + 4 * __popcll(eb2);  // extra pairs (uniform)
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    pl[pp++] = (uint16_t)((lane << 3) | __builtin_ctz(r));
+                    r &= r - 1u;
+                }
+        }
+        const bool any0 = __ballot(fmask != 0u) != 0ull;
+        const int nx = (etot + kWave - 1) / kWave;
+        // a walk whose ticks have needed extra slots for a while (its paths stay
+        // apart: a heavy walk, the launch's tail) takes the SIMD's issue
+        // priority over the light walks beside it (round 4, profiles/r04_ab)
+        fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
+        if ((tt & 7) == 7) {
+            if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#ifdef SGMM_STAMPS
+        lite_sl += (any0 ? 1 : 0) + nx;
+        if (tt == 7) lite_s8 = lite_sl;
+        if (tt == 15) lite_s16 = lite_sl;
+        lite_ts += (any0 ? 4 : 0) + (etot + 15) / 16;
+#endif
+        // the tick's plane rows (tick-offset-major: row u of an episode's block
+        // holds the 64 chunks' rewards at offset u, so a merged wave's store is
+        // one coalesced 512-byte row); a uniform base, the plane stride opaque
+        // per tick so the compiler keeps one address, not one per plane
+        int64_t prs = ep.rs;
+        asm volatile("" : "+s"(prs));
+        const uint64_t pa = reinterpret_cast<uint64_t>(rew + rbase);
+        uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32)) << 32) |
+                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa);
+        asm volatile("" : "+s"(pu));
+        double* const prow = reinterpret_cast<double*>(pu) + frontier_row(tt, 0);
+        uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
+        uint32_t trm = 0;                 // bit f: a fill from frontier state f
+        if (any0) {
+            const bool has = fmask != 0u;
+            const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
+            *reinterpret_cast<f32x4*>(&hb[lane * 4]) = f32x4{s1, s2, (float)(inv_min + (int)f) * 0.5f, 0.0f};
+            float o0, o1;
+            double tmid, task, tbid, tbmax, tsmin;
+            // this tick's prices, requested after layer 2 (out of the register
+            // peak), their latency hidden by layer 3
+            mlp(IntC<4>{}, o0, o1, [&] {
+                tmid = tk.mid_next[tcur];
+                task = tk.best_ask[tcur];
+                tbid = tk.best_bid[tcur];
+                tbmax = tk.buy_max[tcur];
+                tsmin = tk.sell_min[tcur];
+            });
+            if (etot) {
+                px[0][lane] = tmid;
+                px[1][lane] = task;
+                px[2][lane] = tbid;
+                px[3][lane] = tbmax;
+                px[4][lane] = tsmin;
+            }
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
+            if (has) {
+                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
+                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
+                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
+                // the reward goes to the plane of every tracked start whose path
+                // is at f; after the merge only plane p0 is read
+                if (merged) {
+                    prow[p0 * prs + lane] = so1.reward;
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NSI; ++s)
+                        if (((sset >> s) & 1u) && map_get(cur, (uint32_t)s) == f) prow[s * prs + lane] = so1.reward;
+                }
+            }
+        }
+#pragma unroll 1
+        for (int x = 0; x < nx; ++x) {
+            // column lane = pair 64 x + lane: (chunk src, state f)
+            const int pidx = kWave * x + lane;
+            const bool has = pidx < etot;
+            const uint32_t v = has ? (uint32_t)pl[pidx] : 0u;
+            const int src = (int)(v >> 3);
+            const uint32_t f = v & 7u;
+            const f32x2 sg = *reinterpret_cast<const f32x2*>(&sig[src][0]);
+            *reinterpret_cast<f32x4*>(&hb[lane * 4]) = f32x4{sg[0], sg[1], (float)(inv_min + (int)f) * 0.5f, 0.0f};
+            const int ntile = min(4, (etot - kWave * x + 15) >> 4);
+            float o0, o1;
+            if (ntile == 1)
+                mlp(IntC<1>{}, o0, o1, [] {});
+            else if (ntile == 2)
+                mlp(IntC<2>{}, o0, o1, [] {});
+            else
+                mlp(IntC<4>{}, o0, o1, [] {});
+            // the FPT step with the pair's chunk's prices
+            const double smid = px[0][src], sask = px[1][src], sbid = px[2][src], sbmax = px[3][src];
+            const double ssmin = px[4][src];
+            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, smid, sask, sbid, sbmax, ssmin);
+            const uint64_t scur = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cur >> 32), src, kWave) << 32) |
+                                  (uint32_t)__shfl((int)(uint32_t)cur, src, kWave);
+            if (has) {
+                // the pair's chunk is unmerged (a merged chunk has one state): every
+                // tracked start of chunk src whose path is at f
+                const uint32_t ss = cg * kFrontierLanes + src == 0 ? 1u << (uint32_t)(-inv_min) : all;
+#pragma unroll
+                for (int s = 0; s < NSI; ++s)
+                    if (((ss >> s) & 1u) && map_get(scur, (uint32_t)s) == f) prow[s * prs + src] = so1.reward;
+                const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
+                pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
+            }
+        }
+        if (etot) {
+            // the owner lane collects its extra states' successors and fills
+            uint32_t r = ext;
+            int pp = epfx;
+#pragma unroll
+            for (int m = 0; m < NSI - 1; ++m)
+                if (r) {
+                    const uint32_t f = (uint32_t)__builtin_ctz(r);
+                    r &= r - 1u;
+                    const uint32_t w = pl[pp++];
+                    stepmap = (stepmap & ~(0xFFull << (8 * f))) | ((uint64_t)((w >> 9) & 7u) << (8 * f));
+                    trm |= ((w >> 12) & 1u) << f;
+                }
+        }
+        // the trade counts along the tracked paths, the paths' new states
+        if (act) {
+            if (merged) {
+                mcnt += trm != 0u;
+            } else {
+#pragma unroll
+                for (int s = 0; s < NSI; ++s)
+                    if ((sset >> s) & 1u) cnt[s >> 1] += ((trm >> map_get(cur, (uint32_t)s)) & 1u) << (16 * (s & 1));
+            }
+            cur = map_then(cur, stepmap);
+            if (!merged) {
+                uint32_t fm = 0;
+#pragma unroll
+                for (int s = 0; s < NSI; ++s)
+                    if ((sset >> s) & 1u) fm |= 1u << map_get(cur, (uint32_t)s);
+                if (__builtin_popcount(fm) <= 1) {
+                    merged = true;
+                    kc = tt + 1;
+                }
+            }
+        }
+    }
+#ifdef SGMM_STAMPS
+    {
+        unsigned long long t1;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
+        unsigned h_, x_;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(h_), "=s"(x_));
+        const int srow = e + cg * 16384;
+        if (lane == 0 && srow < 32768) {
+            g_tstamps[srow][0] = lite_t0;
+            g_tstamps[srow][1] = t1;
+            g_tstamps[srow][2] = lite_sl;
+            g_tstamps[srow][3] = lite_ts;
+            g_tstamps[srow][6] = lite_s8;
+            g_tstamps[srow][7] = lite_s16;
+            g_thwid[srow][0] = h_;
+            g_thwid[srow][1] = x_;
+        }
+    }
+#endif
+    if (c < nch) {
+        // untracked start states keep the identity byte (never on the episode's path)
+        uint64_t cm = kIdentityMap;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s)
+            if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
+        const int64_t ci = frontier_rec(e, nw, c);
+        cmaps[ci] = cm;
+#pragma unroll
+        for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = ((cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu) + (((sset >> s) & 1u) ? mcnt : 0u);
+        kinfo[ci] = (uint32_t)kc | (p0 << 29);
+    }
+}
+
 int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, hipStream_t s, const FrontierArgs& fa) {
     const dim3 grid(n_waves), block(kWave);
-    if (hidden == 16) {
+    static const bool r4 = [] {
+        const char* v = std::getenv("SGMM_FRONTIER_KERNEL");
+        return v && std::strcmp(v, "r4") == 0;
+    }();
+    if (r4) {  // A/B against round 4's kernel (temporary)
+        if (hidden == 16) {
+            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier_r4<16, 5>), grid, block, 0, s, fa);
+            else SGMM_LAUNCH((k_policy_frontier_r4<16, 8>), grid, block, 0, s, fa);
+        } else {
+            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier_r4<32, 5>), grid, block, 0, s, fa);
+            else SGMM_LAUNCH((k_policy_frontier_r4<32, 8>), grid, block, 0, s, fa);
+        }
+    } else if (hidden == 16) {
         if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier<16, 5>), grid, block, 0, s, fa);
         else SGMM_LAUNCH((k_policy_frontier<16, 8>), grid, block, 0, s, fa);
     } else {

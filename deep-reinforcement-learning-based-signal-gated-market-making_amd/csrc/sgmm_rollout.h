@@ -148,8 +148,12 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
 }
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
 constexpr int kFrPrioExtra = 160;      // a walk's issue priority from 0.625 extra slots per tick on average
-constexpr int kFrontierMaxWaves = 4;   // waves (64-chunk groups) per episode
-constexpr int kFrontierRecs = kFrontierLanes * kFrontierMaxWaves;  // chunk records per episode: e * 256 + c
+constexpr int kFrontierMaxWaves = 16;  // waves (64-chunk groups) per episode
+// the chunk records (map, trade counts, merge info) of an episode cut into nw
+// groups: 64 nw per episode, chunk c of episode e at e * 64 nw + c
+__host__ __device__ __forceinline__ int64_t frontier_rec(int e, int nw, int c) {
+    return (int64_t)e * kFrontierLanes * nw + c;
+}
 constexpr int64_t kFrontierMaxLen = (int64_t)kFrontierLanes * 65532;  // ticks: chunks (multiples of 4) below 2^16 ticks, 16-bit trade counts
 typedef __attribute__((address_space(3))) const float lds_cf;
 typedef __attribute__((address_space(3))) const f32x4 lds_cf4;
@@ -160,13 +164,13 @@ __host__ __device__ __forceinline__ int frontier_len(int T, int nw) {
 }
 // the episode's block of plane rows: nw groups of frontier_len(T, nw) x 64 rows
 // <= T + 256 nw rows (T rounded up to 64 nw chunks of a multiple of 4),
-// starting on a 128-byte line (16 rows), so blocks at step_off + 1040 e
-// (rounded up to 16) never overlap and no two episodes share a line; the plane
-// stride covers total_steps + 1040 n (rew_stride).  Group g's rows start at
-// base + g * CL * 64 (frontier_row within the group)
-constexpr int kFrontierPad = 4 * kFrontierRecs + 16;  // plane rows per episode beyond its ticks
-__device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e) {
-    return (step_off + (int64_t)kFrontierPad * e + 15) & ~int64_t(15);
+// starting on a 128-byte line (16 rows), so blocks at step_off + pad e
+// (rounded up to 16, pad = 256 nw + 16) never overlap and no two episodes
+// share a line; the plane stride covers total_steps + pad n (rew_stride).
+// Group g's rows start at base + g * CL * 64 (frontier_row within the group)
+__host__ __device__ __forceinline__ int64_t frontier_pad(int nw) { return 256LL * nw + 16; }
+__device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e, int nw) {
+    return (step_off + frontier_pad(nw) * e + 15) & ~int64_t(15);
 }
 // Within a group's block, the reward of chunk (lane) l at tick offset u: rows
 // of the 64 chunks at one tick offset (u * 64 + l) -- a walk's store of one

@@ -1282,7 +1282,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     const int CL = FR ? frontier_len(T, nw) : kChunk;
     const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
-    const int64_t cb = FR ? (int64_t)e * kFrontierRecs : (int64_t)chunk_base(so, e);
+    const int64_t cb = FR ? frontier_rec(e, nw, 0) : (int64_t)chunk_base(so, e);
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
     SGMM_STAMP(e, 0);
     if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
@@ -1337,7 +1337,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
                     const uint32_t ki = kin[c];
                     const int kc = (int)(ki & 0x1FFFFFFFu);
                     const int64_t pst = start[c], pp0 = ki >> 29;
-                    const int64_t rb = frontier_base(so, e) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
+                    const int64_t rb = frontier_base(so, e, nw) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        frontier_row(u, c % kFrontierLanes);
 #pragma unroll
                     for (int j = 0; j < kSumTpt; ++j) {
@@ -1410,10 +1410,13 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
     int32_t* __restrict__ trades_out, StepArgs step) {
     extern __shared__ __align__(16) unsigned char lds[];
     __shared__ SumLds<NT> L;
-    __shared__ uint8_t start[FR ? kFrontierRecs : kMaxLen / kChunk];
-    __shared__ uint32_t kin[FR ? kFrontierRecs : 1];
+    __shared__ uint8_t start_t[FR ? 1 : kMaxLen / kChunk];
     __shared__ int red_trades;
     const int e = blockIdx.x;
+    // frontier chunks (64 per group): their start states and merge info follow
+    // the window in the dynamic LDS (scan_lds_bytes)
+    uint8_t* start = FR ? lds + NT * kSumTpt * sizeof(double) : start_t;
+    uint32_t* kin = reinterpret_cast<uint32_t*>(lds + NT * kSumTpt * sizeof(double) + kFrontierLanes * ep.ngrp);
     const ScanShared<NT> sh{reinterpret_cast<double*>(lds), &L, start, kin, &red_trades, lds};
     scan_episode<NSM, NT, FR, TPB>(e, FR ? ep.ngrp : 1, ep, params, inv_min, cmaps, ctr, kinfo, rew, fitness, trades_out,
                                    step, (int)gridDim.x, sh);
@@ -1787,12 +1790,50 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
     return SGMM_OK;
 }
 
-// plane stride: every tick plus the frontier layout's 528 padding rows per episode
-static int64_t rew_stride(int64_t steps, int64_t n) { return (steps + kFrontierPad * n + 31) & ~int64_t(31); }
+// Chunk groups per episode in the frontier kernel (one wave each).  A walk's
+// time is set by its serial chain of ticks, not by its SIMD's load, so when the
+// launch has fewer than two walks per SIMD the episodes are cut into 2-4
+// groups of 64 chunks of proportionally fewer ticks;
+// each extra group pays for tracking every start state of its chunks until
+// their paths merge.  SGMM_FRONTIER_NW=1..16 forces the count (records and
+// plane padding are laid out for the launch's count, frontier_rec / frontier_pad).
+constexpr int kFrontierAutoWaves = 4;  // the default rule's cap
+static int simd_count() {
+    static int n = 0;
+    if (n == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        n = 4 * cus;
+    }
+    return n;
+}
+static int32_t frontier_groups(int32_t n) {
+    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
+        const int g = std::atoi(v);
+        if (g >= 1 && g <= kFrontierMaxWaves) return g;
+    }
+    if (n <= 0) return 1;
+    // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
+    // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups; 256 and 64
+    // episodes: 4 groups fastest, profiles/r04_ab)
+    const int64_t slots = 2LL * simd_count();
+    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, slots / n));
+}
+
+
+// plane stride: every tick, plus (no adversary: the frontier kernel may run)
+// the frontier layout's padding rows per episode, frontier_pad(G) with G the
+// launch's chunk groups; the adversary planes are table rows only
+static int64_t rew_stride(int64_t steps, int32_t n, bool arl) {
+    const int64_t pad = arl ? 0 : frontier_pad(frontier_groups(n)) * n;
+    return (steps + pad + 31) & ~int64_t(31);
+}
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps, e->n), e->order, 1};
+                    e->param, rew_stride(e->total_steps, e->n, with_adv), e->order, 1};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -1827,14 +1868,16 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
 //   no adversary: u64 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
-//                 slots) | f64 path planes rew[n_states][rs] (rs = total_steps
-//                 rounded up to 32)
-//   adversary:    u64 fills[total_steps] | f64 rew[total_steps][n_states]
-//   (frontier kernel: cmaps / ctr hold u64 maps / u32[8] trade counts at slots
-//   e * 128 + c, then u32 kinfo[n * 128] and u32 waves[n] -- each episode's
-//   wave count; the sections are sized for both)
+//                 slots) | u32 kinfo[n * 64 G] | f64 path planes
+//                 rew[n_states][rs] (rs = total_steps + frontier_pad(G) n,
+//                 rounded up to 32; G = frontier_groups(n))
+//   adversary:    u64 fills[total_steps] | f64 rew[n_states][rs] (rs =
+//                 total_steps rounded up to 32)
+//   (frontier kernel: cmaps / ctr hold u64 maps / u32[8] trade counts at the
+//   records e * 64 G + c, kinfo the merge tick | p0 << 29 of each record; the
+//   sections are sized for both the table and the frontier layout)
 static size_t n_chunk_slots(int32_t n, int64_t steps) { return (size_t)steps / kChunk + (size_t)n + 1; }
-static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierRecs; }  // chunk records
+static size_t n_frontier_slots(int32_t n) { return (size_t)n * kFrontierLanes * frontier_groups(n); }  // chunk records
 static size_t ws_cmaps(int32_t n, int64_t steps) {
     return align256(std::max(n_chunk_slots(n, steps), n_frontier_slots(n)) * sizeof(uint64_t));
 }
@@ -1852,9 +1895,9 @@ static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(u
 static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t nsi, bool arl) {
     if (total_steps < 0 || nsi <= 0 || nsi > 8 || n_episodes < 0) return 0;
     if (arl)  // fill codes, per-state planes rew[state * rs + row]
-        return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes) * (size_t)(4 * nsi) * sizeof(double);
+        return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes, true) * (size_t)(4 * nsi) * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           (size_t)rew_stride(total_steps, n_episodes) * (size_t)nsi * sizeof(double);
+           (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
 }
 
 extern "C" size_t sgmm_rollout_workspace_bytes(int32_t n_episodes, int64_t total_steps, int32_t n_inventory,
@@ -1893,36 +1936,6 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
         return m && std::atoi(m) > 0 ? std::atoi(m) : kFrontierMinEps;
     }();
     return eps->n >= min_eps;
-}
-
-// Chunk groups per episode in the frontier kernel (one wave each).  A walk's
-// time is set by its serial chain of ticks, not by its SIMD's load, so when the
-// launch has fewer than two walks per SIMD the episodes are cut into 2-4
-// groups of 64 chunks of proportionally fewer ticks;
-// each extra group pays for tracking every start state of its chunks until
-// their paths merge.  SGMM_FRONTIER_NW=1..4 forces the count.
-static int simd_count() {
-    static int n = 0;
-    if (n == 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-            cus = 256;
-        n = 4 * cus;
-    }
-    return n;
-}
-static int32_t frontier_groups(int32_t n) {
-    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
-        const int g = std::atoi(v);
-        if (g >= 1 && g <= kFrontierMaxWaves) return g;
-    }
-    if (n <= 0) return 1;
-    // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
-    // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups; 256 and 64
-    // episodes: 4 groups fastest, profiles/r04_ab)
-    const int64_t slots = 2LL * simd_count();
-    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierMaxWaves, slots / n));
 }
 
 template <int H>
@@ -2102,6 +2115,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         // instead of idling the CU (A/B on MI355X: P=64 / 256 / 1024 / 4096)
         const int nt = scan_threads(eps->n);
         size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double);  // the window
+        if (fr) lds += (size_t)5 * kFrontierLanes * ep.ngrp;  // chunk start states + merge info
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
         if (fr) {
             if (nsi <= 5)

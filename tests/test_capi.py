@@ -67,9 +67,10 @@ def test_argument_errors_need_no_gpu(sgmm):
         assert rc == -1 and b"genome too large" in L.sgmm_last_error()
     # no adversary: u64 chunk maps + chunk trade counts + frontier merge info + f64 path planes,
     # 256-aligned sections sized for both the table (1000/64 + 4 + 1 chunk slots) and the
-    # frontier kernel (256 chunk records per episode -- up to 4 groups of 64 chunks: u64 map,
-    # u32[8] counts, u32 merge info) (planes: 1000 ticks + 1040 padding rows per episode of
-    # the frontier layout -- 128-byte aligned episode blocks -- rounded to 32)
+    # frontier kernel (64 G chunk records per episode -- G = 4 groups of 64 chunks at 4
+    # episodes: u64 map, u32[8] counts, u32 merge info) (planes: 1000 ticks + 256 G + 16
+    # padding rows per episode of the frontier layout -- 128-byte aligned episode blocks --
+    # rounded to 32)
     assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 256 * 8 + 4 * 256 * 32 + 4 * 256 * 4
                                                          + 5 * 5184 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
@@ -81,16 +82,19 @@ def test_argument_errors_need_no_gpu(sgmm):
                             ctypes.c_void_p(8), ctypes.c_void_p(8), 5000, None)
     assert rc == -1 and b"bars per day" in L.sgmm_last_error()
     # adversary (20 states): u64 fill words + per-state f64 reward planes (stride
-    # 1000 + 1040 * 4 rounded to 32); the scan derives the chunk transducers itself
-    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 20 * 5184 * 8
+    # 1000 rounded to 32: table rows only, no frontier padding); the scan derives
+    # the chunk transducers itself
+    assert L.sgmm_rollout_workspace_size(4, 1000, 20) == 8192 + 20 * 1024 * 8
     # ABI 4: the adversary flag is explicit, so 1 or 2 inventory values (4 or 8
     # states) get the adversary layout, not the no-adversary one of the same state count
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 1) == L.sgmm_rollout_workspace_size(4, 1000, 20)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) == L.sgmm_rollout_workspace_size(4, 1000, 5)
     for nsi in (1, 2):
-        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 4 * nsi * 5184 * 8
-    # the worked example: one 5000-tick ARL episode with 2 inventory values
-    assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) > L.sgmm_rollout_workspace_size(1, 5000, 8)
+        assert L.sgmm_rollout_workspace_bytes(4, 1000, nsi, 1) == 8192 + 4 * nsi * 1024 * 8
+    # the worked example: one 5000-tick ARL episode with 2 inventory values (8
+    # states) has the adversary layout, not the 8-inventory no-adversary one
+    assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) == 40192 + 8 * 5024 * 8
+    assert L.sgmm_rollout_workspace_bytes(1, 5000, 2, 1) != L.sgmm_rollout_workspace_size(1, 5000, 8)
     assert L.sgmm_rollout_workspace_bytes(4, 1000, 9, 0) == 0  # more than 8 inventory values
 
 

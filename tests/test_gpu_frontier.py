@@ -17,10 +17,11 @@ pytestmark = [pytest.mark.gpu,
 DEV = torch.device("cuda:0")
 
 
-@pytest.fixture(params=[1, 2, 3, 4], ids=["1wave", "2waves", "3waves", "4waves"])
+@pytest.fixture(params=[1, 2, 3, 4, 8, 16], ids=["1wave", "2waves", "3waves", "4waves", "8waves", "16waves"])
 def frontier(monkeypatch, request):
-    """The frontier kernel with the episodes cut into 1-4 chunk groups (one
-    wave of 64 chunks each, chunks of frontier_len(T, groups) ticks)."""
+    """The frontier kernel with the episodes cut into 1-16 chunk groups (one
+    wave of 64 chunks each, chunks of frontier_len(T, groups) ticks; records
+    e * 64 G + c, plane padding 256 G + 16 rows per episode)."""
     monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
     monkeypatch.setenv("SGMM_FRONTIER_NW", str(request.param))
 
@@ -202,7 +203,7 @@ def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mod
         assert np.array_equal(out["table"][key], out["frontier"][key], equal_nan=True), key
 
 
-@pytest.mark.parametrize("nw", ["1", "2", "4"], ids=["1wave", "2waves", "4waves"])
+@pytest.mark.parametrize("nw", ["1", "2", "4", "8", "16"], ids=["1wave", "2waves", "4waves", "8waves", "16waves"])
 def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
     """Above 512 episodes the path scan is one wave per episode (1024-tick
     windows of a 256-thread layout run by 64 lanes): chunk lengths from 4 to

@@ -205,17 +205,19 @@ def test_bench_config_population(sgmm, oracle):
     assert np.array_equal(fit, want_f)
 
 
-@pytest.mark.parametrize("caps", [(2, -2), (3, -4)], ids=["5states", "8states"])
-@pytest.mark.parametrize("n_ep", [400, 600, 1100])
-def test_many_episode_scan(sgmm, oracle, n_ep, caps):
+@pytest.mark.parametrize("n_ep,caps,H", [(n, c, 16) for n in (400, 600, 1100) for c in ((2, -2), (3, -4))] +
+                         [(n, (2, -2), h) for n in (600, 1100) for h in (8, 64)])
+def test_many_episode_scan(sgmm, oracle, n_ep, caps, H):
     """More than 256 / 512 episodes take the 8-wave / one-wave path scan (2048- /
-    1024-tick windows; 400 episodes run the table, 600 and 1100 the frontier
-    kernel): ragged lengths around their window boundaries, every
-    episode bit-exact; with 5 inventory states (the default caps) and with 8
-    (i_max=3, i_min=-4: the NSM=8 scan instantiations)."""
+    1024-tick windows; at H=16 400 episodes run the table, 600 and 1100 the
+    frontier kernel; H=8 and H=64 have no frontier kernel, so 600 and 1100
+    episodes take the table path into the one-wave scan): ragged lengths around
+    their window boundaries, every episode bit-exact; with 5 inventory states
+    (the default caps) and with 8 (i_max=3, i_min=-4: the NSM=8 scan
+    instantiations)."""
     i_max, i_min = caps
     from sgmm_amd import synthetic
-    T, H = 5000, 16
+    T = 5000
     base = [0, 1, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3600, 4096, 5000]
     lens = np.array([base[i % len(base)] if i < 96 else 700 + (37 * i) % 4300 for i in range(n_ep)], np.int64)
     P = len(lens)
