@@ -75,8 +75,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     uint32_t* __restrict__ ctr32 = args.ctr32;
     uint32_t* __restrict__ kinfo = args.kinfo;
     double* __restrict__ rew = args.rew;
-    const int nw = ep.ngrp;
-    const int pos = (int)blockIdx.x / nw, cg = (int)blockIdx.x - pos * nw;
+    int pos, cg, nw;  // order position, chunk group, the episode's groups
+    frontier_wave(ep, (int)blockIdx.x, pos, cg, nw);
     const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int64_t rbase = frontier_base(so, e, nw) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int64_t rbase = frontier_base(so, e, ep.ngrp) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
     const int t0 = c * CL;
     const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
 
@@ -529,11 +529,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = frontier_rec(e, nw, c);
+        const int64_t ci = frontier_rec(e, ep.ngrp, c);
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
-        kinfo[ci] = (uint32_t)kc | (p0 << 29);
+        kinfo[ci] = (uint32_t)kc | ((uint32_t)nw << 20) | (p0 << 29);
     }
 }
 
@@ -569,6 +569,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
     __shared__ __attribute__((aligned(16))) float c1s[NT][4][4];   // layer-1 C: [hf][g][r] = b1[16 hf + 4r + g]
     __shared__ __attribute__((aligned(16))) float b2s[H];
+#ifdef SGMM_L1_VALU
+    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], W1[k][2], b1[k])
+#endif
     __shared__ __attribute__((aligned(8))) float sig[kWave][2];    // the tick's signals of each chunk
     __shared__ double px[5][kWave];  // the tick's prices of each chunk (for the extra slots' FPT steps)
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
@@ -584,8 +587,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     uint32_t* __restrict__ ctr32 = args.ctr32;
     uint32_t* __restrict__ kinfo = args.kinfo;
     double* __restrict__ rew = args.rew;
-    const int nw = ep.ngrp;
-    const int pos = (int)blockIdx.x / nw, cg = (int)blockIdx.x - pos * nw;
+    int pos, cg, nw;  // order position, chunk group, the episode's groups
+    frontier_wave(ep, (int)blockIdx.x, pos, cg, nw);
     const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
@@ -595,7 +598,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const int c = cg * kFrontierLanes + lane;          // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int64_t rbase = frontier_base(so, e, nw) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
+    const int64_t rbase = frontier_base(so, e, ep.ngrp) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
     const int t0 = c * CL;
     const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
 
@@ -607,6 +610,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     if (lane < H) {
         b2s[lane] = gsm[L::B2 + lane];
         c1s[lane >> 4][lane & 3][(lane >> 2) & 3] = gsm[L::B1 + lane];  // neuron lane = 16 hf + 4 r + g
+#ifdef SGMM_L1_VALU
+        l1w[lane][0] = gsm[L::W1 + 3 * lane];
+        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
+        l1w[lane][2] = gsm[L::W1 + 3 * lane + 2];
+        l1w[lane][3] = gsm[L::B1 + lane];
+#endif
     }
     // A of layer 1, lane (g, col): W1[16 hf + 4 (col % 4) + col / 4][g], 0 at g = 3
     float a1[NT];
@@ -642,6 +651,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_s8 = 0, lite_s16 = 0;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
 #endif
+#ifdef SGMM_STAMPS_PHASE
+    // per wave: 0 cycles, 1 layers 1-2 (MFMA issue), 2 layer-2 drain + transpose
+    // + layer 3, 4 FPT step + plane stores, 5 per-tick head, 6 tick tail,
+    // 3 slots run, 7 wall time (10 ns ticks)
+    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
+#define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");
+    SGMM_FT(fs_t0);
+#define SGMM_PH(k)                    \
+    do {                              \
+        unsigned long long t_;        \
+        SGMM_FT(t_);                  \
+        fs_c[k] += t_ - fs_b;         \
+        fs_b = t_;                    \
+    } while (0)
+#else
+#define SGMM_PH(k) \
+    do {           \
+    } while (0)
+#endif
     int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
     int fr_extra = 0;
@@ -661,6 +690,33 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         for (int q0 = 0; q0 < NQ; q0 += 2) {
             constexpr int Q2 = NQ < 2 ? NQ : 2;
             f32x4 h1[Q2][NT];
+#ifdef SGMM_L1_VALU
+            // layer 1 on the vector ALU, two columns per v_pk_fma_f32 (each half
+            // a single-rounding fma: the canonical chain b1 + w0 s1 + w1 s2 + w2 x2)
+            {
+                f32x4 in[Q2];
+#pragma unroll
+                for (int q = 0; q < Q2; ++q) in[q] = *reinterpret_cast<const f32x4*>(&hb[(16 * (q0 + q) + col) * 4]);
+                lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
+                asm volatile("" : "+v"(l1p));
+#pragma unroll
+                for (int i = 0; i < KS; ++i) {
+                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
+                    if constexpr (Q2 == 2) {
+                        f32x2 pv = __builtin_elementwise_fma(f32x2{w[0], w[0]}, f32x2{in[0][0], in[1][0]}, f32x2{w[3], w[3]});
+                        pv = __builtin_elementwise_fma(f32x2{w[1], w[1]}, f32x2{in[0][1], in[1][1]}, pv);
+                        pv = __builtin_elementwise_fma(f32x2{w[2], w[2]}, f32x2{in[0][2], in[1][2]}, pv);
+                        h1[0][i >> 2][i & 3] = relu(pv[0]);
+                        h1[1][i >> 2][i & 3] = relu(pv[1]);
+                    } else {
+                        float a = __builtin_fmaf(w[0], in[0][0], w[3]);
+                        a = __builtin_fmaf(w[1], in[0][1], a);
+                        a = __builtin_fmaf(w[2], in[0][2], a);
+                        h1[0][i >> 2][i & 3] = relu(a);
+                    }
+                }
+            }
+#else
 #pragma unroll
             for (int hf = 0; hf < NT; ++hf) {
                 const f32x4 cc = *reinterpret_cast<const f32x4*>(&c1s[hf][grp][0]);
@@ -674,6 +730,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                 for (int hf = 0; hf < NT; ++hf)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) h1[q][hf][r] = relu(h1[q][hf][r]);
+#endif
 #pragma unroll
             for (int rt = 0; rt < NT; ++rt) {
                 const f32x4 bb = *reinterpret_cast<const f32x4*>(&b2s[16 * rt + 4 * grp]);
@@ -689,6 +746,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                         acc[q0 + q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[q][i >> 2][i & 3],
                                                                               acc[q0 + q][rt], 0, 0, 0);
         }
+        SGMM_PH(1);
         after_layer2();
         asm volatile("" ::: "memory");  // the input rows are read before the transpose overwrites them
         o0 = w3i[2 * H];
@@ -722,10 +780,17 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             }
             asm volatile("" ::: "memory");  // this half's rows are read before the next half is written
         }
+#ifdef SGMM_STAMPS_PHASE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+        SGMM_PH(2);
     };
 
 #pragma unroll 1
     for (int tt = 0; tt < CL; ++tt) {
+#ifdef SGMM_STAMPS_PHASE
+        SGMM_FT(fs_b);
+#endif
         const bool act = tt < ntl;
         const float s1 = ns1, s2 = ns2;
         const int64_t tcur = ti;
@@ -791,6 +856,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         double* const prow = reinterpret_cast<double*>(pu) + frontier_row(tt, 0);
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
         uint32_t trm = 0;                 // bit f: a fill from frontier state f
+#ifdef SGMM_STAMPS_PHASE
+        fs_c[3] += (any0 ? 1 : 0) + nx;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+        SGMM_PH(5);
         if (any0) {
             const bool has = fmask != 0u;
             const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
@@ -830,6 +900,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                         if (((sset >> s) & 1u) && map_get(cur, (uint32_t)s) == f) prow[s * prs + lane] = so1.reward;
                 }
             }
+#ifdef SGMM_STAMPS_PHASE
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+            SGMM_PH(4);
         }
 #pragma unroll 1
         for (int x = 0; x < nx; ++x) {
@@ -867,6 +941,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                 const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
                 pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
             }
+#ifdef SGMM_STAMPS_PHASE
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+            SGMM_PH(4);
         }
         if (etot) {
             // the owner lane collects its extra states' successors and fills
@@ -903,8 +981,26 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                 }
             }
         }
+#ifdef SGMM_STAMPS_PHASE
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#endif
+        SGMM_PH(6);
     }
-#ifdef SGMM_STAMPS
+#ifdef SGMM_STAMPS_PHASE
+    {
+        unsigned long long t_, r1;
+        SGMM_FT(t_);
+        fs_c[0] = t_ - fs_t0;
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
+        if (lane == 0 && e < kStampWaves) {
+            for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
+            g_tstamps[e][7] = r1 - fs_r0;
+        }
+    }
+#undef SGMM_FT
+#endif
+#undef SGMM_PH
+#if defined(SGMM_STAMPS) && !defined(SGMM_STAMPS_PHASE)
     {
         unsigned long long t1;
         asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
@@ -929,11 +1025,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s)
             if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = frontier_rec(e, nw, c);
+        const int64_t ci = frontier_rec(e, ep.ngrp, c);
         cmaps[ci] = cm;
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = ((cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu) + (((sset >> s) & 1u) ? mcnt : 0u);
-        kinfo[ci] = (uint32_t)kc | (p0 << 29);
+        kinfo[ci] = (uint32_t)kc | ((uint32_t)nw << 20) | (p0 << 29);
     }
 }
 

@@ -23,10 +23,13 @@ struct EpArrays {
     const int32_t* param;
     int64_t rs;  // no adversary: reward table stride, rew[state * rs + row] (SoA)
     const int32_t* order;  // frontier kernel: episode of order position p (NULL: p)
-    // frontier kernel: every episode of the launch is cut into ngrp groups of
-    // 64 chunks, one wave each (chunks of frontier_len(T, ngrp) ticks); the
-    // path scan derives the same chunk layout from it
+    // frontier kernel: the episodes at order positions [0, whole) are cut into
+    // g0 groups of 64 chunks (one wave each, chunks of frontier_len(T, g0)
+    // ticks), the rest into gtail groups (frontier_plan); ngrp = the larger,
+    // the layout of the records (64 ngrp per episode) and plane padding; the
+    // path scan reads an episode's group count from its first record
     int32_t ngrp;
+    int32_t g0, gtail, whole;
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or
@@ -181,6 +184,25 @@ __device__ __forceinline__ int64_t frontier_base(int64_t step_off, int e, int nw
 __host__ __device__ __forceinline__ int64_t frontier_row(int u, int l) {
     return (int64_t)u * kFrontierLanes + l;
 }
+// wave b of a frontier launch -> the order position it walks, its chunk group
+// and the episode's group count (EpArrays::g0 / gtail / whole)
+__device__ __forceinline__ void frontier_wave(const EpArrays& ep, int b, int& pos, int& cg, int& nw) {
+    const int nb0 = ep.whole * ep.g0;
+    if (b < nb0) {
+        pos = b / ep.g0;
+        cg = b - pos * ep.g0;
+        nw = ep.g0;
+    } else {
+        const int j = b - nb0, q = j / ep.gtail;
+        pos = ep.whole + q;
+        cg = j - q * ep.gtail;
+        nw = ep.gtail;
+    }
+}
+// chunk record merge info: the merge tick offset (bits 0-15), the episode's
+// group count (bits 20-24), the lowest tracked start state (bits 29-31)
+constexpr uint32_t kKinfoTick = 0xFFFFu;
+__host__ __device__ __forceinline__ uint32_t kinfo_groups(uint32_t k) { return (k >> 20) & 31u; }
 
 // ------------------------------------------------------------------ frontier kernel launch
 struct FrontierArgs {

@@ -1279,10 +1279,13 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     uint8_t* start = sh.start;
     uint32_t* kin = sh.kin;
     const int32_t T = ep.len[e];
-    const int CL = FR ? frontier_len(T, nw) : kChunk;
-    const int nch = (T + CL - 1) / CL;
     const int64_t so = ep.step_off[e];
+    // FR: records laid out for nw (ep.ngrp) groups; the episode's own group
+    // count is in its first record
     const int64_t cb = FR ? frontier_rec(e, nw, 0) : (int64_t)chunk_base(so, e);
+    const int nwe = (FR && T > 0) ? (int)kinfo_groups(kinfo[cb]) : 1;
+    const int CL = FR ? frontier_len(T, nwe) : kChunk;
+    const int nch = (T + CL - 1) / CL;
     const int tid = threadIdx.x, lane = tid & (kWave - 1);
     SGMM_STAMP(e, 0);
     if (tid < kWave) {  // chunk start states, 64 chunks per round, carried across rounds
@@ -1335,7 +1338,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
                 if (FR) {  // plane of the start state before the chunk's paths merge, plane p0 after
                     const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
                     const uint32_t ki = kin[c];
-                    const int kc = (int)(ki & 0x1FFFFFFFu);
+                    const int kc = (int)(ki & kKinfoTick);
                     const int64_t pst = start[c], pp0 = ki >> 29;
                     const int64_t rb = frontier_base(so, e, nw) + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
                                        frontier_row(u, c % kFrontierLanes);
@@ -1809,18 +1812,52 @@ static int simd_count() {
     }
     return n;
 }
-static int32_t frontier_groups(int32_t n) {
+// The launch's chunk-group plan: g0 groups for the episodes at order positions
+// [0, whole), gtail groups for the rest; gmax = the record / padding layout.
+struct FrontierPlan {
+    int32_t g0, gtail, whole, gmax;
+    int64_t waves;
+};
+static FrontierPlan frontier_plan(int32_t n) {
+    FrontierPlan p{1, 1, std::max(n, 0), 1, std::max<int64_t>(n, 0)};
     if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
         const int g = std::atoi(v);
-        if (g >= 1 && g <= kFrontierMaxWaves) return g;
+        if (g >= 1 && g <= kFrontierMaxWaves) {
+            p.g0 = p.gtail = p.gmax = g;
+            p.waves = (int64_t)n * g;
+            return p;
+        }
     }
-    if (n <= 0) return 1;
+    if (n <= 0) return p;
     // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
     // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups; 256 and 64
     // episodes: 4 groups fastest, profiles/r04_ab)
-    const int64_t slots = 2LL * simd_count();
-    return (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, slots / n));
+    const int64_t S = simd_count();
+    p.g0 = p.gtail = p.gmax = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, 2 * S / n));
+    // Whole walks are dispatched one per SIMD per run of S waves, so n = a S + r
+    // leaves r SIMDs with a walk more than the others, and the walks on those
+    // SIMDs end last.  The r episodes at the end of the order are cut into
+    // ~S / r groups instead: the last run of waves becomes ~S shorter walks,
+    // one per SIMD (config 3: 2560 = 2 x 1024 + 512 -> 2048 whole walks and
+    // 512 episodes in 2 groups, every SIMD 2.5 episodes' work).
+    // SGMM_FRONTIER_TAIL=0 keeps every walk whole.
+    static const bool tail = [] {
+        const char* v = std::getenv("SGMM_FRONTIER_TAIL");
+        return !(v && std::strcmp(v, "0") == 0);
+    }();
+    const int64_t r = n % S;
+    if (tail && p.g0 == 1 && n > S && r > 0) {
+        const int64_t gt = std::max<int64_t>(1, std::min<int64_t>(kFrontierMaxWaves, (S + r / 2) / r));
+        if (gt > 1) {
+            p.whole = (int32_t)(n - r);
+            p.gtail = p.gmax = (int32_t)gt;
+        }
+    }
+    p.waves = (int64_t)p.whole * p.g0 + (int64_t)(n - p.whole) * p.gtail;
+    return p;
 }
+// the record / plane-padding layout of a launch of n episodes
+static int32_t frontier_groups(int32_t n) { return frontier_plan(n).gmax; }
 
 
 // plane stride: every tick, plus (no adversary: the frontier kernel may run)
@@ -1833,7 +1870,7 @@ static int64_t rew_stride(int64_t steps, int32_t n, bool arl) {
 
 static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
     return EpArrays{e->genome, with_adv ? e->adv : nullptr, e->tick_off, e->len, e->step_off,
-                    e->param, rew_stride(e->total_steps, e->n, with_adv), e->order, 1};
+                    e->param, rew_stride(e->total_steps, e->n, with_adv), e->order, 1, 1, 1, e->n};
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -2061,7 +2098,13 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     EpArrays ep = ep_arrays(eps, arl);
     const bool fr = use_frontier(arl, hidden, eps);
-    if (fr) ep.ngrp = frontier_groups(eps->n);
+    const FrontierPlan plan = frontier_plan(eps->n);
+    if (fr) {
+        ep.ngrp = plan.gmax;
+        ep.g0 = plan.g0;
+        ep.gtail = plan.gtail;
+        ep.whole = plan.whole;
+    }
     const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || arl || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (hidden 16 or 32) or the adversary path", eps->max_len,
@@ -2072,7 +2115,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
         const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
                               kinfo, rew};
-        if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)eps->n * (unsigned)ep.ngrp, s, fa)) return rc;
+        if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, s, fa)) return rc;
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);

@@ -270,11 +270,19 @@ class _GraphedGenerations:
                         fn()
                     self.graphs.append(g)
         if self.full_graph and self.graph_batch > 1 and self.batch_graph is None:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(self.graph_batch):
-                    self._gen()
-            self.batch_graph = g
+            # batches of graph_batch, graph_batch / 2, ..., 2 generations: any
+            # generation count replays as at most log2(graph_batch) + 1 graphs,
+            # never as a train of single-generation replays paced by the host
+            self.batch_graphs = {}
+            B = self.graph_batch
+            while B > 1:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(B):
+                        self._gen()
+                self.batch_graphs[B] = g
+                B //= 2
+            self.batch_graph = self.batch_graphs[self.graph_batch]
 
     def step(self, gen: int):
         """Enqueue generation ``gen`` (drl_engine.py:92-171) on the current stream."""
@@ -299,10 +307,10 @@ class _GraphedGenerations:
             for g in range(gen0, gen0 + n):
                 self.step(g)
             return
-        B, done = self.graph_batch, 0
-        if B > 1 and n >= B:
+        done = 0
+        for B in sorted(self.batch_graphs, reverse=True):
             while n - done >= B:
-                self.batch_graph.replay()
+                self.batch_graphs[B].replay()
                 done += B
         for g in range(gen0 + done, gen0 + n):
             self.step(g)
@@ -407,7 +415,7 @@ class TrainingSession(_GraphedGenerations):
         # generation on one rank; with several ranks the rollout and the boundary
         # are captured separately around the (eager) all-gather
         self.use_graph = bool(eng.use_graph) and not self.torch_rng
-        self.graphs, self.batch_graph, self.full_graph = None, None, False
+        self.graphs, self.batch_graph, self.batch_graphs, self.full_graph = None, None, {}, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, eng.sync_every))
         self.roll.reserve(self.train_eps, arl)
         if self.val_eps is not None:
@@ -730,7 +738,7 @@ class MultiSession(_GraphedGenerations):
                                      self.masters_adv.data_ptr() if arl else None, self.best_masters.data_ptr(),
                                      self.seeds.data_ptr(), self.hist.data_ptr())
         self.use_graph = bool(e0.use_graph)
-        self.graphs, self.batch_graph, self.full_graph = None, None, False
+        self.graphs, self.batch_graph, self.batch_graphs, self.full_graph = None, None, {}, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, e0.sync_every))
         self.roll.reserve(self.eps, arl)
         if self.val_eps is not None:
