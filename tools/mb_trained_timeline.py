@@ -129,3 +129,16 @@ for lo in range(0, n, 1024):
     print(f"  blocks {lo}-{hi - 1}: {len(su)} distinct SIMDs, {len(np.unique(sid[lo:hi] // 4))} distinct CUs")
 order = np.argsort(s0, kind="stable")
 print("  first 16 blocks: (XCD, SE, CU, SIMD)", [(int(xcc[b]), int(se[b]), int(cu[b]), int(simd[b])) for b in range(16)])
+# early slot counts (slots in the first 8 / 16 ticks) as heaviness probes
+s8 = h[:, 6].astype(float)
+s16 = h[:, 7].astype(float)
+whole = sl > 60  # whole walks (split halves have ~half the ticks)
+for name, pr in (("s8", s8), ("s16", s16)):
+    x, y = pr[whole], sl[whole]
+    top = y >= np.percentile(y, 95)
+    print(f"  {name}: percentiles 50/90/95/99 {[float(np.percentile(x, q)) for q in (50, 90, 95, 99)]}; corr with total "
+          f"{np.corrcoef(x, y)[0, 1]:.2f}; top-5% walks' {name} med {np.median(x[top]):.0f} min {x[top].min():.0f}")
+    for thr in np.percentile(x, [80, 90, 95]):
+        sel = x >= thr
+        print(f"    {name} >= {thr:.0f}: selects {sel.sum()} walks, catches {np.sum(sel & top)} of {top.sum()} top-5%;"
+              f" their total slots med {np.median(y[sel]):.0f}")
