@@ -894,6 +894,18 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
 #pragma unroll
         for (int j = 0; j < kSumBlk; ++j) allz &= r[j] == 0.0;
         const int32_t be = allz ? kZeroRun : (fast && !bad && !edge) ? eb : INT32_MIN;
+#ifdef SGMM_STAMPS
+        {   // why blocks have no prediction: [6] += no binade | bad step << 20 | binade edge << 40, [7] += zero blocks
+            const unsigned long long nf = __popcll(__ballot(live && !allz && !fast));
+            const unsigned long long nb = __popcll(__ballot(live && !allz && fast && bad));
+            const unsigned long long ne = __popcll(__ballot(live && !allz && fast && !bad && edge));
+            const unsigned long long nz = __popcll(__ballot(live && allz));
+            if (lane == 0 && blockIdx.x < 4096) {
+                atomicAdd(&g_stamps[blockIdx.x][6], nf | nb << 20 | ne << 40);
+                atomicAdd(&g_stamps[blockIdx.x][7], nz);
+            }
+        }
+#endif
         // block sums -> wave-local exclusive prefix zl
         const uint64_t zinc = wave_scan_add((uint64_t)P);
         const int64_t zl = (int64_t)(zinc - (uint64_t)P);
@@ -1320,7 +1332,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
     // per episode, summed over the windows: 11 gather cycles, 12 sum cycles,
     // 15 windows; 13 / 14 walk iterations / fallback blocks
     unsigned long long sw_a, sw_b, sw_g = 0, sw_s = 0, sw_n = 0;
-    if (tid == 0 && e < 4096) g_stamps[e][13] = g_stamps[e][14] = 0;
+    if (tid == 0 && e < 4096) g_stamps[e][13] = g_stamps[e][14] = g_stamps[e][6] = g_stamps[e][7] = 0;
 #define SGMM_SW(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
 #endif
     double S = 0.0;  // exact running sum (identical in every thread between windows)
@@ -1800,7 +1812,7 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
 // each extra group pays for tracking every start state of its chunks until
 // their paths merge.  SGMM_FRONTIER_NW=1..16 forces the count (records and
 // plane padding are laid out for the launch's count, frontier_rec / frontier_pad).
-constexpr int kFrontierAutoWaves = 4;  // the default rule's cap
+constexpr int kFrontierAutoWaves = 8;  // the default rule's cap
 static int simd_count() {
     static int n = 0;
     if (n == 0) {
@@ -1830,10 +1842,13 @@ static FrontierPlan frontier_plan(int32_t n) {
     }
     if (n <= 0) return p;
     // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
-    // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups; 256 and 64
-    // episodes: 4 groups fastest, profiles/r04_ab)
+    // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups, round 4;
+    // 270 / 272 / 331 us at 2 / 4 / 8 groups, round 5), four from half as many
+    // episodes as SIMDs down (the 1-of-16 shard, 512 episodes: 236 / 203 / 185 us
+    // at 2 / 4 / 8 groups, profiles/r05_small)
     const int64_t S = simd_count();
-    p.g0 = p.gtail = p.gmax = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, 2 * S / n));
+    const int64_t per = n <= S / 2 ? 4 : 2;
+    p.g0 = p.gtail = p.gmax = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, per * S / n));
     // Whole walks are dispatched one per SIMD per run of S waves, so n = a S + r
     // leaves r SIMDs with a walk more than the others, and the walks on those
     // SIMDs end last.  The r episodes at the end of the order are cut into

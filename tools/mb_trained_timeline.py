@@ -62,6 +62,33 @@ eng2 = sg.RolloutEngine(DEV)
 for _ in range(3):
     eng2.fitness(ticks, eps, params, pop, H)
 torch.cuda.synchronize()
+if os.environ.get("SCAN"):
+    # the path scan of the same launch (SGMM_STAMP slots, as tools/mb_scan3_stamps.py)
+    L.sgmm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    g_ = np.zeros((n, 16), np.uint64)
+    L.sgmm_debug_stamps(g_.ctypes.data, n)
+    g_ = g_.astype(np.int64)
+    tot = (g_[:, 3] - g_[:, 0]).astype(float)
+    print(f"scan, trained {G_TRAIN} generations: entry->end cycles p10 {np.percentile(tot, 10):.0f} med "
+          f"{np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f} max {tot.max():.0f}; "
+          f"span {(g_[:, 3].max() - g_[:, 0].min()):.0f}")
+    ga, sm, it, fb = g_[:, 11], g_[:, 12], g_[:, 13], g_[:, 14]
+    print(f"  per episode: chunk starts med {np.median(g_[:, 1] - g_[:, 0]):.0f}, gather med {np.median(ga):.0f}, "
+          f"exact sum med {np.median(sm):.0f}, walk iterations med {np.median(it):.0f}, fallback blocks med "
+          f"{np.median(fb):.0f}")
+    why = g_[:, 6].astype(np.uint64)
+    nf, nb, ne = (why & 0xFFFFF).astype(float), ((why >> 20) & 0xFFFFF).astype(float), (why >> 40).astype(float)
+    print(f"  blocks without a prediction per episode (med / p90): no binade {np.median(nf):.0f}/{np.percentile(nf, 90):.0f}, "
+          f"bad step {np.median(nb):.0f}/{np.percentile(nb, 90):.0f}, binade edge {np.median(ne):.0f}/"
+          f"{np.percentile(ne, 90):.0f}; zero blocks {np.median(g_[:, 7]):.0f}")
+    o = np.argsort(tot)[::-1]
+    print("  slowest (e, entry->end, gather, sum, iters, fallbacks):",
+          [(int(e), int(tot[e]), int(ga[e]), int(sm[e]), int(it[e]), int(fb[e])) for e in o[:10]])
+    for q in (50, 90, 99):
+        m_ = tot >= np.percentile(tot, q)
+        print(f"  >= p{q}: fallbacks {fb[m_].mean():.1f} iters {it[m_].mean():.1f} sum {sm[m_].mean():.0f} "
+              f"gather {ga[m_].mean():.0f}")
+    sys.exit(0)
 h = np.zeros((n, 8), np.uint64)
 L.sgmm_debug_frontier_tstamps(h.ctypes.data, n)
 if PHASE:
