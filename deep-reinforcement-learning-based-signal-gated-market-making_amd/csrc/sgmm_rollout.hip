@@ -1853,15 +1853,24 @@ static FrontierPlan frontier_plan(int32_t n) {
     // leaves r SIMDs with a walk more than the others, and the walks on those
     // SIMDs end last.  The r episodes at the end of the order are cut into
     // ~S / r groups instead: the last run of waves becomes ~S shorter walks,
-    // one per SIMD (config 3: 2560 = 2 x 1024 + 512 -> 2048 whole walks and
-    // 512 episodes in 2 groups, every SIMD 2.5 episodes' work).
+    // one per SIMD (1536 = 1024 + 512 -> 1024 whole walks and 512 episodes in 2
+    // groups; config 3's 2560 = 2 x 1024 + 512 -> 2048 + 512 in 2 groups took
+    // the policy kernel from 547 to 525 us, before the four-walk rule below).
     // SGMM_FRONTIER_TAIL=0 keeps every walk whole.
     static const bool tail = [] {
         const char* v = std::getenv("SGMM_FRONTIER_TAIL");
         return !(v && std::strcmp(v, "0") == 0);
     }();
     const int64_t r = n % S;
-    if (tail && p.g0 == 1 && n > S && r > 0) {
+    if (tail && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
+        // from 2.5 episodes per SIMD up to 4: four walks per SIMD, 2n - 4S whole
+        // and the rest in halves, one whole and three half walks per SIMD (config
+        // 3: 2560 = 1024 whole + 1536 in halves; 660.5-668.0 against 670.3-670.6 us
+        // per generation for 2048 whole + 512 in halves, and 690-699 us for all in
+        // halves, profiles/r05_ab/ab20_*, ab21_*)
+        p.whole = (int32_t)(2 * n - 4 * S);
+        p.gtail = p.gmax = 2;
+    } else if (tail && p.g0 == 1 && n > S && r > 0) {
         const int64_t gt = std::max<int64_t>(1, std::min<int64_t>(kFrontierMaxWaves, (S + r / 2) / r));
         if (gt > 1) {
             p.whole = (int32_t)(n - r);
