@@ -150,7 +150,10 @@ __device__ __forceinline__ int mbcnt64(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 constexpr int kFrontierLanes = 64;     // chunks per wave (one per lane)
-constexpr int kFrPrioExtra = 160;      // a walk's issue priority from 0.625 extra slots per tick on average
+#ifndef SGMM_FR_PRIO_EXTRA
+#define SGMM_FR_PRIO_EXTRA 160
+#endif
+constexpr int kFrPrioExtra = SGMM_FR_PRIO_EXTRA;  // a walk's issue priority from 0.625 extra slots per tick on average
 constexpr int kFrontierMaxWaves = 16;  // waves (64-chunk groups) per episode
 // the chunk records (map, trade counts, merge info) of an episode cut into nw
 // groups: 64 nw per episode, chunk c of episode e at e * 64 nw + c
