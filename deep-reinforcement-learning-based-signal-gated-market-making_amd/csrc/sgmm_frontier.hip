@@ -39,506 +39,15 @@ __device__ unsigned int g_thwid[kStampWaves][2];  // HW_ID, XCC_ID of each wave
 // the other chunks track every state in [inv_min, inv_max].  Arithmetic per
 // (tick, state) is the table's (same MFMA chains, same fp64 step), so every
 // output bit is the table's.
-// ------------------------------------------------------------------ frontier kernel (the walk)
-
-
-// Wave b walks chunk group cg = b % ngrp of the episode at order position
-// b / ngrp (longest episodes first).  (Round 3's walks with tick hand-offs and
-// the launch with the path scans fused in measured no faster:
-// tools/experiments/round3_opt_in_paths.patch.)
-template <int H, int NSI>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void k_policy_frontier_r4(FrontierArgs args) {
-    static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
-    using L = GenomeLayout<H>;
-    constexpr int NT = H / 16, KS = H / 4;
-    constexpr int HP = H + 4;  // LDS row pitch (floats) of the transposed activations
-    // LDS (~13 KB per wave, so 3 waves per SIMD fit): the genome is staged in
-    // `big`, the weights the loop needs are copied out, then `big` holds the
-    // half-activation transpose buffer and the per-state rewards
-    constexpr int kBig = (L::N * 4 > kWave * HP * 4 + NSI * kWave * 8) ? L::N * 4 : kWave * HP * 4 + NSI * kWave * 8;
-    __shared__ __attribute__((aligned(16))) unsigned char big[kBig];
-    // (13 200 bytes of LDS per wave for H = 32 with `big`: twelve waves fit a
-    // CU's 160 KiB in 512-byte granules; 13 328 bytes allowed only eleven)
-    __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
-    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], b1[k], W1[k][2])
-    __shared__ __attribute__((aligned(16))) float b2s[H];
-    // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
-    // successor (bits 9-11) and the fill (bit 12) written back by the column
-    __shared__ uint16_t pl[kWave * (NSI - 1)];
-
-    const sgmm_ticks& tk = args.tk;
-    const EpArrays& ep = args.ep;
-    const sgmm_env_params* __restrict__ params = args.params;
-    const GenomeSrc& src = args.src;
-    const int32_t inv_min = args.inv_min, nsi = args.nsi;
-    uint64_t* __restrict__ cmaps = args.cmaps;
-    uint32_t* __restrict__ ctr32 = args.ctr32;
-    uint32_t* __restrict__ kinfo = args.kinfo;
-    double* __restrict__ rew = args.rew;
-    int pos, cg, nw;  // order position, chunk group, the episode's groups
-    frontier_wave(ep, (int)blockIdx.x, pos, cg, nw);
-    const int e = ep.order ? ep.order[pos] : pos;
-    const int32_t T = ep.len[e];
-    if (T <= 0) return;  // block-uniform
-    const int CL = frontier_len(T, nw);
-    const int nch = (T + CL - 1) / CL;
-    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
-    const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
-    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
-    const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
-    const int64_t rbase = frontier_base(so, e, ep.ngrp) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
-    const int t0 = c * CL;
-    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
-
-    float* gsm = reinterpret_cast<float*>(big);
-    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
-    __syncthreads();
-    if (lane < 2 * H) w3i[lane] = gsm[L::W3 + (lane & 1) * H + (lane >> 1)];
-    if (lane < 2) w3i[2 * H + lane] = gsm[L::B3 + lane];
-    if (lane < H) {
-        l1w[lane][0] = gsm[L::W1 + 3 * lane];
-        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
-        l1w[lane][2] = gsm[L::B1 + lane];
-        l1w[lane][3] = gsm[L::W1 + 3 * lane + 2];
-        b2s[lane] = gsm[L::B2 + lane];
-    }
-    float w2f[NT][KS];  // A of layer 2: neuron 16rt + col, k = 4i + grp
-#pragma unroll
-    for (int rt = 0; rt < NT; ++rt)
-#pragma unroll
-        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
-    __syncthreads();  // gsm is dead from here: big becomes hb + rl
-    float* hb = reinterpret_cast<float*>(big);                          // [64][HP]
-    double* rl = reinterpret_cast<double*>(big + kWave * HP * 4);       // [NSI][64]
-    const sgmm_env_params p = params[ep.param[e]];
-
-    // per-lane path bookkeeping: byte s of cur = the state of the path that
-    // started the chunk in state s (tracked starts: bits of sset)
-    const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
-    const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
-    uint64_t cur = kIdentityMap;
-    // trade count along the path from each tracked start: 16 bits per start,
-    // two per word (a chunk has < 2^16 ticks: kFrontierMaxLen)
-    uint32_t cnt[(NSI + 1) / 2];
-#pragma unroll
-    for (int s = 0; s < (NSI + 1) / 2; ++s) cnt[s] = 0;
-    bool merged = __builtin_popcount(sset) <= 1;
-    int kc = merged ? 0 : CL;  // merge offset (CL: never)
-    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
-#ifdef SGMM_STAMPS
-    // timeline build: realtime at start (slot 0) and end (slot 1), HW_ID / XCC_ID,
-    // slots and tile-slots run (slots 2, 3); nothing inside the loop waits
-    unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_pk = 0, lite_pt = 0, lite_s8 = 0, lite_s16 = 0;
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
-#endif
-#ifdef SGMM_STAMPS_PHASE
-    // per wave (episode): 0 cycles, 1 layers 1-2 (MFMA issue), 2 relu + transpose
-    // (MFMA drain), 3 layer 3, 4 FPT step, 5 per-tick head (frontier, signals,
-    // layer-1 terms), 6 planes, 7 wall time (10 ns ticks)
-    unsigned long long fs_t0, fs_a, fs_b, fs_c[7] = {0, 0, 0, 0, 0, 0, 0}, fs_r0;
-#define SGMM_FT(var) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory")
-    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(fs_r0)::"memory");  // 100 MHz
-    SGMM_FT(fs_t0);
-#endif
-    int64_t ti = tick_of(0);
-    float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
-    int fr_extra = 0;
-#pragma unroll 1
-    for (int tt = 0; tt < CL; ++tt) {
-#ifdef SGMM_STAMPS_PHASE
-        SGMM_FT(fs_a);
-#endif
-        const bool act = tt < ntl;
-        const float s1 = ns1, s2 = ns2;
-        // this tick's prices: first used after the tick's MLP, which hides the load
-        const double tmid = tk.mid_next[ti], task = tk.best_ask[ti], tbid = tk.best_bid[ti];
-        const double tbmax = tk.buy_max[ti], tsmin = tk.sell_min[ti];
-        ti = tick_of(tt + 1);
-        ns1 = tk.s1n[ti];
-        ns2 = tk.s2n[ti];
-        // frontier: the distinct current states of the tracked paths
-        uint32_t fmask = 0;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s)
-            if ((sset >> s) & 1u) fmask |= 1u << map_get(cur, (uint32_t)s);
-        if (!act) fmask = 0;
-#ifdef SGMM_STAMPS
-        {
-            // what (chunk, state) pairs packed densely into the 64 columns would need
-            int so = __builtin_popcount(fmask);
-#pragma unroll
-            for (int m = 32; m >= 1; m >>= 1) so += __shfl_xor(so, m, kWave);
-            lite_pk += (so + 63) / 64;
-            lite_pt += (so + 15) / 16;
-        }
-#endif
-        // the weights stay in LDS: an opaque base per tick keeps the compiler
-        // from hoisting ~90 loop-invariant weight loads into registers
-        lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
-        asm volatile("" : "+v"(l1p));
-        // layer 1's signal terms for the B-operand samples (sample 16q + col = lane 16q + col's tick)
-        float pre[4][KS];
-        // the frontier of each B-operand sample's chunk (lane 16q + col): the
-        // slots take their k-th state from it, no per-slot permute
-        uint32_t remq[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) remq[q] = (uint32_t)__shfl((int)fmask, 16 * q + col, kWave);
-        {
-            float xs0[4], xs1[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                xs0[q] = __shfl(s1, 16 * q + col, kWave);
-                xs1[q] = __shfl(s2, 16 * q + col, kWave);
-            }
-#pragma unroll
-            for (int i = 0; i < KS; ++i) {
-                const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
-#pragma unroll
-                for (int q = 0; q < 4; ++q) pre[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
-            }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        SGMM_FT(fs_b);
-        fs_c[5] += fs_b - fs_a;
-#endif
-        uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
-        uint32_t trm = 0;                 // bit f: a fill from frontier state f
-        // Slot 0: each lane's first frontier state in its own column (the
-        // common case: most ticks have one state per chunk).  Slots 1..: the
-        // remaining (chunk, state) pairs packed densely into the 64 columns --
-        // a chunk whose paths stay apart costs its extra states, not extra
-        // slots for the whole wave.  Each column computes with its pair's own
-        // inputs (the chunk's signals and prices, the state's inventory), so
-        // every (tick, state) result is bit-identical to the unpacked walk.
-        const uint32_t ext = fmask & (fmask - 1u);  // frontier states after the first
-        const uint32_t nex = (uint32_t)__builtin_popcount(ext);
-        const uint64_t eb0 = __ballot(nex & 1u), eb1 = __ballot(nex & 2u), eb2 = __ballot(nex & 4u);
-        const int epfx = mbcnt64(eb0) + 2 * mbcnt64(eb1) + 4 * mbcnt64(eb2);  // first pair of this lane
-        const int etot = __popcll(eb0) + 2 * __popcll(eb1) + 4 * __popcll(eb2);  // extra pairs (uniform)
-        {
-            uint32_t r = ext;
-            int pp = epfx;
-#pragma unroll
-            for (int m = 0; m < NSI - 1; ++m)
-                if (r) {
-                    pl[pp++] = (uint16_t)((lane << 3) | __builtin_ctz(r));
-                    r &= r - 1u;
-                }
-        }
-        const bool any0 = __ballot(fmask != 0u) != 0ull;
-        const int nx = (etot + kWave - 1) / kWave;
-        // a walk whose ticks have needed extra slots for a while (its paths stay
-        // apart: a heavy walk, the launch's tail) takes the SIMD's issue
-        // priority over the light walks beside it (config 3: policy kernel
-        // 560-571 -> 533 us at thresholds 128 and 192, profiles/r04_ab)
-        fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
-#ifndef SGMM_NO_FR_PRIO
-        if ((tt & 7) == 7) {
-            // (graded levels 0-3 at 0.3 / 0.6 / 1.25 extra slots per tick measured
-            // the same: 664-665 vs 664-668 us per config-3 generation, r04ab_*)
-            if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
-#ifdef SGMM_STAMPS
-        lite_sl += (any0 ? 1 : 0) + nx;
-        if (tt == 7) lite_s8 = lite_sl;    // slots run in the first 8 / 16 ticks (heaviness probes)
-        if (tt == 15) lite_s16 = lite_sl;
-        lite_ts += (any0 ? 4 : 0) + (etot + 15) / 16;
-#endif
-        // layers 1-3 of the four 16-column tiles' samples (tiles >= NQ skipped):
-        // x2q / pq = inv / 2 and the layer-1 signal terms of sample 16q + col
-        auto mlp = [&](auto nq, const float(&x2q)[4], const float(&pq)[4][KS], float& o0, float& o1) {
-            constexpr int NQ = decltype(nq)::value;
-            lds_cf* w3p = (lds_cf*)(&w3i[0]);
-            asm volatile("" : "+v"(w3p));
-            lds_cf* w1p = (lds_cf*)(&l1w[0][0]);  // W1[k][2] at l1w[k][3]
-            asm volatile("" : "+v"(w1p));
-            lds_cf* b2p = (lds_cf*)(&b2s[0]);
-            asm volatile("" : "+v"(b2p));
-            // layer 1 + layer 2: 4 x NT independent accumulator chains issued
-            // k-step by k-step keep the matrix pipe busy
-            f32x4 acc[4][NT];
-#pragma unroll
-            for (int rt = 0; rt < NT; ++rt) {
-                const f32x4 bb = *reinterpret_cast<lds_cf4*>(b2p + 16 * rt + 4 * grp);
-#pragma unroll
-                for (int q = 0; q < NQ; ++q) acc[q][rt] = bb;
-            }
-#pragma unroll
-            for (int i4 = 0; i4 < KS; i4 += 4) {
-                float u[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) u[r] = w1p[4 * (4 * (i4 + r) + grp) + 3];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-#pragma unroll
-                    for (int q = 0; q < NQ; ++q) {
-                        const float h1 = relu(__builtin_fmaf(u[r], x2q[q], pq[q][i4 + r]));
-#pragma unroll
-                        for (int rt = 0; rt < NT; ++rt)
-                            acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i4 + r], h1, acc[q][rt], 0, 0, 0);
-                    }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                SGMM_FT(t_);  // MFMAs issued (not completed)
-                fs_c[1] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-#pragma unroll
-            for (int q = 0; q < NQ; ++q)
-#pragma unroll
-                for (int rt = 0; rt < NT; ++rt) {
-                    f32x4 v;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
-                    *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
-                }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[2] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-            // layer 3 of this lane's column, in neuron order (the canonical chain)
-            o0 = w3p[2 * H];
-            o1 = w3p[2 * H + 1];
-#pragma unroll 1
-            for (int j8 = 0; j8 < H / 8; ++j8) {
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int j4 = 2 * j8 + jj;
-                    const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
-#pragma unroll
-                    for (int r2 = 0; r2 < 2; ++r2) {
-                        const f32x4 w = *reinterpret_cast<lds_cf4*>(w3p + 2 * (4 * j4 + 2 * r2));
-                        o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
-                        o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
-                        o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
-                        o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
-                    }
-                }
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[3] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        };
-        if (any0) {
-            float x2q[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t fq = remq[q] ? (uint32_t)__builtin_ctz(remq[q]) : 0u;
-                x2q[q] = (float)(inv_min + (int)fq) * 0.5f;
-            }
-            float o0, o1;
-            mlp(IntC<4>{}, x2q, pre, o0, o1);
-            const bool has = fmask != 0u;
-            const uint32_t f = has ? (uint32_t)__builtin_ctz(fmask) : 0u;
-            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
-            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, tmid, task, tbid, tbmax, tsmin);
-            if (has) {
-                const uint64_t to = (uint64_t)(f + so1.fill_buy - so1.fill_sell);
-                stepmap = (stepmap & ~(0xFFull << (8 * f))) | (to << (8 * f));
-                trm |= (uint32_t)(so1.fill_buy | so1.fill_sell) << f;
-                rl[f * kWave + lane] = so1.reward;
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[4] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        }
-#pragma unroll 1
-        for (int x = 0; x < nx; ++x) {
-            // column lane = pair 64 x + lane: (chunk lane src, state f)
-            const int pidx = kWave * x + lane;
-            const bool has = pidx < etot;
-            const uint32_t v = has ? (uint32_t)pl[pidx] : 0u;
-            const int src = (int)(v >> 3);
-            const uint32_t f = v & 7u;
-            float x2q[4], pq[4][KS];
-            {
-                float xs0[4], xs1[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t vq = (uint32_t)__shfl((int)v, 16 * q + col, kWave);
-                    const int sq = (int)(vq >> 3);
-                    x2q[q] = (float)(inv_min + (int)(vq & 7u)) * 0.5f;
-                    xs0[q] = __shfl(s1, sq, kWave);
-                    xs1[q] = __shfl(s2, sq, kWave);
-                }
-                lds_cf* l1q = (lds_cf*)(&l1w[0][0]);
-                asm volatile("" : "+v"(l1q));
-#pragma unroll
-                for (int i = 0; i < KS; ++i) {
-                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1q + 4 * (4 * i + grp));
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) pq[q][i] = __builtin_fmaf(w[1], xs1[q], __builtin_fmaf(w[0], xs0[q], w[2]));
-                }
-            }
-            const int ntile = min(4, (etot - kWave * x + 15) >> 4);
-            float o0, o1;
-            if (ntile == 1)
-                mlp(IntC<1>{}, x2q, pq, o0, o1);
-            else if (ntile == 2)
-                mlp(IntC<2>{}, x2q, pq, o0, o1);
-            else
-                mlp(IntC<4>{}, x2q, pq, o0, o1);
-            // the FPT step with the pair's chunk's prices
-            const double smid = __shfl(tmid, src, kWave), sask = __shfl(task, src, kWave);
-            const double sbid = __shfl(tbid, src, kWave), sbmax = __shfl(tbmax, src, kWave);
-            const double ssmin = __shfl(tsmin, src, kWave);
-            const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
-            const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
-            const StepOut so1 = ftp_step(p, inv_min + (int)f, oa, ob, smid, sask, sbid, sbmax, ssmin);
-            if (has) {
-                rl[f * kWave + src] = so1.reward;
-                const uint32_t to = f + (uint32_t)so1.fill_buy - (uint32_t)so1.fill_sell;
-                pl[pidx] = (uint16_t)(v | (to << 9) | ((uint32_t)(so1.fill_buy | so1.fill_sell) << 12));
-            }
-#ifdef SGMM_STAMPS_PHASE
-            {
-                unsigned long long t_;
-                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-                SGMM_FT(t_);
-                fs_c[4] += t_ - fs_b;
-                fs_b = t_;
-            }
-#endif
-        }
-        {
-            // the owner lane collects its extra states' successors and fills
-            uint32_t r = ext;
-            int pp = epfx;
-#pragma unroll
-            for (int m = 0; m < NSI - 1; ++m)
-                if (r) {
-                    const uint32_t f = (uint32_t)__builtin_ctz(r);
-                    r &= r - 1u;
-                    const uint32_t w = pl[pp++];
-                    stepmap = (stepmap & ~(0xFFull << (8 * f))) | ((uint64_t)((w >> 9) & 7u) << (8 * f));
-                    trm |= ((w >> 12) & 1u) << f;
-                }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        SGMM_FT(fs_b);
-#endif
-        // the tick's rewards along the tracked paths; once they have merged only plane p0
-        if (act) {
-            // planes in tick-offset-major order (row u of an episode's block holds
-            // the 64 chunks' rewards at offset u): one coalesced 512-byte store
-            // per plane and tick; row-major rows made every 8-byte store a
-            // partial line and the L2 wrote ~6x the bytes back
-            // plane s's row: one per-lane base plus a uniform offset (the plane
-            // stride made opaque per tick, so the compiler keeps one 64-bit
-            // address, not one per plane: that saved the registers of four)
-            int64_t prs = ep.rs;
-            asm volatile("" : "+s"(prs));
-            // uniform: the group's first row (readfirstlane: e came from a load)
-            const uint64_t pa = reinterpret_cast<uint64_t>(rew + rbase);
-            uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32)) << 32) |
-                          (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa);
-            asm volatile("" : "+s"(pu));
-            double* const prow = reinterpret_cast<double*>(pu);
-            const int64_t toff = frontier_row(tt, 0);  // uniform; lane l at + frontier_row(0, l)
-#pragma unroll
-            for (int s = 0; s < NSI; ++s) {
-                if (!((sset >> s) & 1u)) continue;
-                const uint32_t st = map_get(cur, (uint32_t)s);
-                if (!merged || (uint32_t)s == p0) prow[s * prs + toff + frontier_row(0, lane)] = rl[st * kWave + lane];
-                cnt[s >> 1] += ((trm >> st) & 1u) << (16 * (s & 1));
-            }
-            cur = map_then(cur, stepmap);
-            if (!merged) {
-                uint32_t fm = 0;
-#pragma unroll
-                for (int s = 0; s < NSI; ++s)
-                    if ((sset >> s) & 1u) fm |= 1u << map_get(cur, (uint32_t)s);
-                if (__builtin_popcount(fm) <= 1) {
-                    merged = true;
-                    kc = tt + 1;
-                }
-            }
-        }
-#ifdef SGMM_STAMPS_PHASE
-        {
-            unsigned long long t_;
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-            SGMM_FT(t_);
-            fs_c[6] += t_ - fs_b;
-        }
-#endif
-    }
-#ifdef SGMM_STAMPS_PHASE
-    {
-        unsigned long long t_;
-        SGMM_FT(t_);
-        fs_c[0] = t_ - fs_t0;
-        unsigned long long r1;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(r1)::"memory");
-        if (lane == 0 && e < kStampWaves) {
-            for (int k = 0; k < 7; ++k) g_tstamps[e][k] = fs_c[k];
-            g_tstamps[e][7] = r1 - fs_r0;  // wall time in 10 ns ticks: the shader clock = [0] / [7]
-        }
-    }
-#undef SGMM_FT
-#endif
-#if defined(SGMM_STAMPS) && !defined(SGMM_STAMPS_PHASE)
-    {
-        unsigned long long t1;
-        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
-        unsigned h_, x_;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)" : "=s"(h_), "=s"(x_));
-        const int srow = e + cg * 16384;  // a split episode's second group: row e + 16384
-        if (lane == 0 && srow < 32768) {
-            g_tstamps[srow][0] = lite_t0;
-            g_tstamps[srow][1] = t1;
-            g_tstamps[srow][2] = lite_sl;
-            g_tstamps[srow][3] = lite_ts;
-            g_tstamps[srow][4] = lite_pk;
-            g_tstamps[srow][5] = lite_pt;
-            g_tstamps[srow][6] = lite_s8;
-            g_tstamps[srow][7] = lite_s16;
-            g_thwid[srow][0] = h_;
-            g_thwid[srow][1] = x_;
-        }
-    }
-#endif
-    if (c < nch) {
-        // untracked start states keep the identity byte (never on the episode's path)
-        uint64_t cm = kIdentityMap;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s)
-            if ((sset >> s) & 1u) cm = (cm & ~(0xFFull << (8 * s))) | ((uint64_t)map_get(cur, (uint32_t)s) << (8 * s));
-        const int64_t ci = frontier_rec(e, ep.ngrp, c);
-        cmaps[ci] = cm;
-#pragma unroll
-        for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = (cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
-        kinfo[ci] = (uint32_t)kc | ((uint32_t)nw << 20) | (p0 << 29);
-    }
-}
-
-// ------------------------------------------------------------------ frontier kernel (round 5)
-// The same walk, with each slot's MLP restructured for the SIMD's pipes
+//
+// Wave b walks a chunk group of the episode at an order position (longest
+// episodes first; frontier_wave maps b by the launch plan).  (Round 3's walks
+// with tick hand-offs and the launch with the path scans fused in measured no
+// faster: tools/experiments/round3_opt_in_paths.patch; round 5's helper waves
+// and tile offers neither: tools/experiments/round5_tile_offers.patch.  Round 4's
+// kernel, three waves per SIMD, is in the round-4 commits.)
+//
+// Each slot's MLP is laid out for the SIMD's pipes
 // (tools/mb/mb_xwave3.hip: one wave's vector ops do not overlap its own MFMAs,
 // but another wave's float ops run beside them at full rate):
 //   - layer 1 on the matrix core: per 16-column tile q and neuron half hf one
@@ -555,7 +64,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(3))) void
 //   - a lane whose paths have merged keeps one trade count and stores its
 //     slot-0 reward straight from the register.
 // <= 128 VGPRs and <= 10 KB of LDS (H = 32, 5 states): four walks per SIMD.
-template <int H, int NSI>
+// LS: waves per 64-chunk group (lane split).  With LS > 1 each wave walks
+// 64 / LS of the group's chunks (lanes past them idle): the same chunks, the
+// same chunk starts, LS times the waves -- for launches with fewer walks than
+// the SIMDs hold.
+template <int H, int NSI, int LS>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_policy_frontier(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
@@ -569,9 +82,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     __shared__ __attribute__((aligned(16))) float w3i[2 * H + 2];  // (W3[0][j], W3[1][j]) pairs, then b3
     __shared__ __attribute__((aligned(16))) float c1s[NT][4][4];   // layer-1 C: [hf][g][r] = b1[16 hf + 4r + g]
     __shared__ __attribute__((aligned(16))) float b2s[H];
-#ifdef SGMM_L1_VALU
-    __shared__ __attribute__((aligned(16))) float l1w[H][4];       // (W1[k][0], W1[k][1], W1[k][2], b1[k])
-#endif
     __shared__ __attribute__((aligned(8))) float sig[kWave][2];    // the tick's signals of each chunk
     __shared__ double px[5][kWave];  // the tick's prices of each chunk (for the extra slots' FPT steps)
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
@@ -587,20 +97,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     uint32_t* __restrict__ ctr32 = args.ctr32;
     uint32_t* __restrict__ kinfo = args.kinfo;
     double* __restrict__ rew = args.rew;
+    static_assert(LS == 1 || LS == 2 || LS == 4, "lane split 1, 2 or 4");
+    constexpr int NL = kFrontierLanes / LS;  // chunks (lanes) this wave walks
     int pos, cg, nw;  // order position, chunk group, the episode's groups
-    frontier_wave(ep, (int)blockIdx.x, pos, cg, nw);
+    frontier_wave(ep, (int)blockIdx.x / LS, pos, cg, nw);
+    const int off = ((int)blockIdx.x % LS) * NL;  // this wave's first chunk within the group
     const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
     if (T <= 0) return;  // block-uniform
     const int CL = frontier_len(T, nw);
     const int nch = (T + CL - 1) / CL;
-    if (cg * kFrontierLanes >= nch) return;  // a group past the episode's last chunk
+    if (cg * kFrontierLanes + off >= nch) return;  // a group (part) past the episode's last chunk
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
-    const int c = cg * kFrontierLanes + lane;          // this lane's chunk
+    const bool lane_ok = LS == 1 || lane < NL;
+    const int c = cg * kFrontierLanes + off + lane;    // this lane's chunk
     const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
     const int64_t rbase = frontier_base(so, e, ep.ngrp) + (int64_t)cg * CL * kFrontierLanes;  // the group's rows
     const int t0 = c * CL;
-    const int ntl = max(0, min(T, t0 + CL) - t0);      // its ticks (0 past the last chunk)
+    const int ntl = lane_ok ? max(0, min(T, t0 + CL) - t0) : 0;  // its ticks (0 past the last chunk)
 
     float* gsm = reinterpret_cast<float*>(big);
     stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
@@ -610,12 +124,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     if (lane < H) {
         b2s[lane] = gsm[L::B2 + lane];
         c1s[lane >> 4][lane & 3][(lane >> 2) & 3] = gsm[L::B1 + lane];  // neuron lane = 16 hf + 4 r + g
-#ifdef SGMM_L1_VALU
-        l1w[lane][0] = gsm[L::W1 + 3 * lane];
-        l1w[lane][1] = gsm[L::W1 + 3 * lane + 1];
-        l1w[lane][2] = gsm[L::W1 + 3 * lane + 2];
-        l1w[lane][3] = gsm[L::B1 + lane];
-#endif
     }
     // A of layer 1, lane (g, col): W1[16 hf + 4 (col % 4) + col / 4][g], 0 at g = 3
     float a1[NT];
@@ -634,7 +142,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     // per-lane path bookkeeping: byte s of cur = the state of the path that
     // started the chunk in state s (tracked starts: bits of sset)
     const uint32_t all = (1u << nsi) - 1u;
-    const uint32_t sset = c >= nch ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
+    const uint32_t sset = (!lane_ok || c >= nch) ? 0u : (c == 0 ? 1u << (uint32_t)(-inv_min) : all);
     const uint32_t p0 = sset ? (uint32_t)__builtin_ctz(sset) : 0u;
     uint64_t cur = kIdentityMap;
     // trade count along the path from each tracked start until the paths
@@ -646,7 +154,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     uint32_t mcnt = 0;
     bool merged = __builtin_popcount(sset) <= 1;
     int kc = merged ? 0 : CL;  // merge offset (CL: never)
-    auto tick_of = [&](int tt) { return tb + t0 + min(tt, max(ntl - 1, 0)); };
+    // (a split wave's idle lanes read the episode's first tick)
+    auto tick_of = [&](int tt) { return tb + (LS == 1 || ntl > 0 ? t0 : 0) + min(tt, max(ntl - 1, 0)); };
 #ifdef SGMM_STAMPS
     unsigned long long lite_t0, lite_sl = 0, lite_ts = 0, lite_s8 = 0, lite_s16 = 0;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(lite_t0)::"memory");
@@ -690,33 +199,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         for (int q0 = 0; q0 < NQ; q0 += 2) {
             constexpr int Q2 = NQ < 2 ? NQ : 2;
             f32x4 h1[Q2][NT];
-#ifdef SGMM_L1_VALU
-            // layer 1 on the vector ALU, two columns per v_pk_fma_f32 (each half
-            // a single-rounding fma: the canonical chain b1 + w0 s1 + w1 s2 + w2 x2)
-            {
-                f32x4 in[Q2];
-#pragma unroll
-                for (int q = 0; q < Q2; ++q) in[q] = *reinterpret_cast<const f32x4*>(&hb[(16 * (q0 + q) + col) * 4]);
-                lds_cf* l1p = (lds_cf*)(&l1w[0][0]);
-                asm volatile("" : "+v"(l1p));
-#pragma unroll
-                for (int i = 0; i < KS; ++i) {
-                    const f32x4 w = *reinterpret_cast<lds_cf4*>(l1p + 4 * (4 * i + grp));
-                    if constexpr (Q2 == 2) {
-                        f32x2 pv = __builtin_elementwise_fma(f32x2{w[0], w[0]}, f32x2{in[0][0], in[1][0]}, f32x2{w[3], w[3]});
-                        pv = __builtin_elementwise_fma(f32x2{w[1], w[1]}, f32x2{in[0][1], in[1][1]}, pv);
-                        pv = __builtin_elementwise_fma(f32x2{w[2], w[2]}, f32x2{in[0][2], in[1][2]}, pv);
-                        h1[0][i >> 2][i & 3] = relu(pv[0]);
-                        h1[1][i >> 2][i & 3] = relu(pv[1]);
-                    } else {
-                        float a = __builtin_fmaf(w[0], in[0][0], w[3]);
-                        a = __builtin_fmaf(w[1], in[0][1], a);
-                        a = __builtin_fmaf(w[2], in[0][2], a);
-                        h1[0][i >> 2][i & 3] = relu(a);
-                    }
-                }
-            }
-#else
 #pragma unroll
             for (int hf = 0; hf < NT; ++hf) {
                 const f32x4 cc = *reinterpret_cast<const f32x4*>(&c1s[hf][grp][0]);
@@ -730,7 +212,6 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
                 for (int hf = 0; hf < NT; ++hf)
 #pragma unroll
                     for (int r = 0; r < 4; ++r) h1[q][hf][r] = relu(h1[q][hf][r]);
-#endif
 #pragma unroll
             for (int rt = 0; rt < NT; ++rt) {
                 const f32x4 bb = *reinterpret_cast<const f32x4*>(&b2s[16 * rt + 4 * grp]);
@@ -853,7 +334,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         uint64_t pu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32)) << 32) |
                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa);
         asm volatile("" : "+s"(pu));
-        double* const prow = reinterpret_cast<double*>(pu) + frontier_row(tt, 0);
+        double* const prow = reinterpret_cast<double*>(pu) + frontier_row(tt, off);
         uint64_t stepmap = kIdentityMap;  // byte f = successor of frontier state f
         uint32_t trm = 0;                 // bit f: a fill from frontier state f
 #ifdef SGMM_STAMPS_PHASE
@@ -869,7 +350,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             double tmid, task, tbid, tbmax, tsmin;
             // this tick's prices, requested after layer 2 (out of the register
             // peak), their latency hidden by layer 3
-            mlp(IntC<4>{}, o0, o1, [&] {
+            mlp(IntC<NL / 16>{}, o0, o1, [&] {
                 tmid = tk.mid_next[tcur];
                 task = tk.best_ask[tcur];
                 tbid = tk.best_bid[tcur];
@@ -934,7 +415,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
             if (has) {
                 // the pair's chunk is unmerged (a merged chunk has one state): every
                 // tracked start of chunk src whose path is at f
-                const uint32_t ss = cg * kFrontierLanes + src == 0 ? 1u << (uint32_t)(-inv_min) : all;
+                const uint32_t ss = cg * kFrontierLanes + off + src == 0 ? 1u << (uint32_t)(-inv_min) : all;
 #pragma unroll
                 for (int s = 0; s < NSI; ++s)
                     if (((ss >> s) & 1u) && map_get(scur, (uint32_t)s) == f) prow[s * prs + src] = so1.reward;
@@ -1019,7 +500,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         }
     }
 #endif
-    if (c < nch) {
+    if (lane_ok && c < nch) {
         // untracked start states keep the identity byte (never on the episode's path)
         uint64_t cm = kIdentityMap;
 #pragma unroll
@@ -1033,26 +514,24 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     }
 }
 
-int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, hipStream_t s, const FrontierArgs& fa) {
+int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa) {
     const dim3 grid(n_waves), block(kWave);
-    static const bool r4 = [] {
-        const char* v = std::getenv("SGMM_FRONTIER_KERNEL");
-        return v && std::strcmp(v, "r4") == 0;
-    }();
-    if (r4) {  // A/B against round 4's kernel (temporary)
+    {
+        const dim3 gs(n_waves * (unsigned)ls);
+#define SGMM_FR_LAUNCH(H_, N_)                                                                   \
+    do {                                                                                         \
+        if (ls == 4) SGMM_LAUNCH((k_policy_frontier<H_, N_, 4>), gs, block, 0, s, fa);           \
+        else if (ls == 2) SGMM_LAUNCH((k_policy_frontier<H_, N_, 2>), gs, block, 0, s, fa);      \
+        else SGMM_LAUNCH((k_policy_frontier<H_, N_, 1>), grid, block, 0, s, fa);                 \
+    } while (0)
         if (hidden == 16) {
-            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier_r4<16, 5>), grid, block, 0, s, fa);
-            else SGMM_LAUNCH((k_policy_frontier_r4<16, 8>), grid, block, 0, s, fa);
+            if (nsi <= 5) SGMM_FR_LAUNCH(16, 5);
+            else SGMM_FR_LAUNCH(16, 8);
         } else {
-            if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier_r4<32, 5>), grid, block, 0, s, fa);
-            else SGMM_LAUNCH((k_policy_frontier_r4<32, 8>), grid, block, 0, s, fa);
+            if (nsi <= 5) SGMM_FR_LAUNCH(32, 5);
+            else SGMM_FR_LAUNCH(32, 8);
         }
-    } else if (hidden == 16) {
-        if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier<16, 5>), grid, block, 0, s, fa);
-        else SGMM_LAUNCH((k_policy_frontier<16, 8>), grid, block, 0, s, fa);
-    } else {
-        if (nsi <= 5) SGMM_LAUNCH((k_policy_frontier<32, 5>), grid, block, 0, s, fa);
-        else SGMM_LAUNCH((k_policy_frontier<32, 8>), grid, block, 0, s, fa);
+#undef SGMM_FR_LAUNCH
     }
     SGMM_LAUNCHED();
     return SGMM_OK;

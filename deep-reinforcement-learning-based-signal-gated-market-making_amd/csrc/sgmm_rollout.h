@@ -222,6 +222,7 @@ struct FrontierArgs {
 
 // launches the frontier kernel for hidden = 16 / 32 and nsi inventory states
 // (sgmm_frontier.hip): grid = episodes x ep.ngrp waves
-int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, hipStream_t s, const FrontierArgs& fa);
+// ls: waves per 64-chunk group (1, 2 or 4; the grid is n_waves x ls)
+int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa);
 
 }  // namespace sgmm

@@ -1828,10 +1828,15 @@ static int simd_count() {
 // [0, whole), gtail groups for the rest; gmax = the record / padding layout.
 struct FrontierPlan {
     int32_t g0, gtail, whole, gmax;
-    int64_t waves;
+    int64_t waves;  // walks (64-chunk groups)
+    int32_t ls;     // waves per walk (lane split, k_policy_frontier<H, NSI, LS>)
 };
 static FrontierPlan frontier_plan(int32_t n) {
-    FrontierPlan p{1, 1, std::max(n, 0), 1, std::max<int64_t>(n, 0)};
+    FrontierPlan p{1, 1, std::max(n, 0), 1, std::max<int64_t>(n, 0), 1};
+    if (const char* v = std::getenv("SGMM_FRONTIER_LS")) {  // experiments: waves per walk
+        const int l = std::atoi(v);
+        if (l == 2 || l == 4) p.ls = l;
+    }
     if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
         const int g = std::atoi(v);
         if (g >= 1 && g <= kFrontierMaxWaves) {
@@ -1843,12 +1848,15 @@ static FrontierPlan frontier_plan(int32_t n) {
     if (n <= 0) return p;
     // two walks per SIMD (measured, config 5's 1-of-8 shard, 1024 episodes of
     // 3600 ticks: 317 / 274 / 313 / 336 us at 1 / 2 / 3 / 4 groups, round 4;
-    // 270 / 272 / 331 us at 2 / 4 / 8 groups, round 5), four from half as many
-    // episodes as SIMDs down (the 1-of-16 shard, 512 episodes: 236 / 203 / 185 us
-    // at 2 / 4 / 8 groups, profiles/r05_small)
+    // 270 / 272 / 331 us at 2 / 4 / 8 groups, round 5; splitting lanes instead,
+    // 283-311 us, profiles/r05_small)
     const int64_t S = simd_count();
-    const int64_t per = n <= S / 2 ? 4 : 2;
-    p.g0 = p.gtail = p.gmax = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, per * S / n));
+    p.g0 = p.gtail = p.gmax = (int32_t)std::max<int64_t>(1, std::min<int64_t>(kFrontierAutoWaves, 2 * S / n));
+    // from half as many episodes as SIMDs down, two waves per walk (lane split):
+    // four waves per SIMD without more chunk starts (the 1-of-16 shard, 512
+    // episodes: frontier + scan 248.5 us at G = 4 with two waves per walk against
+    // 255.9 us at G = 8 and 270.6 us at G = 4 with one, profiles/r05_small/ls_*, c5s16_fr4)
+    if (n <= S / 2 && p.ls == 1 && !std::getenv("SGMM_FRONTIER_LS")) p.ls = 2;
     // Whole walks are dispatched one per SIMD per run of S waves, so n = a S + r
     // leaves r SIMDs with a walk more than the others, and the walks on those
     // SIMDs end last.  The r episodes at the end of the order are cut into
@@ -2139,7 +2147,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
         const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
                               kinfo, rew};
-        if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, s, fa)) return rc;
+        if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, plan.ls, s, fa)) return rc;
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);

@@ -217,3 +217,20 @@ def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=51, sigma=0.3)
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
+
+
+@pytest.mark.parametrize("ls,nw", [("2", "1"), ("2", "4"), ("4", "1"), ("4", "3")],
+                         ids=["2waves_1group", "2waves_4groups", "4waves_1group", "4waves_3groups"])
+@pytest.mark.parametrize("H", [16, 32])
+def test_frontier_lane_split(sgmm, oracle, monkeypatch, ls, nw, H):
+    """Lane split (k_policy_frontier<H, NSI, LS>): two or four waves per 64-chunk
+    walk, each walking 32 or 16 of its chunks (the default from S/2 episodes
+    down); ragged lengths, every group count, 5 and 8 states -- bit-exact."""
+    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
+    monkeypatch.setenv("SGMM_FRONTIER_LS", ls)
+    monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
+    lens = [0, 1, 5, 63, 65, 257, 1000, 4097, 4560, 9001]
+    for caps in ((2, -2), (3, -4)):
+        fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=71, caps=caps, sigma=0.5)
+        assert np.array_equal(trd, wt), caps
+        assert np.array_equal(fit, wf), caps

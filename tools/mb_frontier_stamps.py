@@ -47,10 +47,8 @@ for name, sl, T in (("train", slice(0, P), 4560), ("val", slice(P, P + NV), 912)
     print(f"{name}: T={T} chunk={CL} waves={len(x)}")
     print(f"  cycles/wave {med(x[:, 0]):9.0f}   per tick {med(x[:, 0]) / CL:7.0f}   wall {med(x[:, 7]) / 100:8.1f} us"
           f"   shader clock {med(x[:, 0] / np.maximum(x[:, 7], 1)) / 10:6.3f} GHz")
-    labs = (((1, "layer 1-2"), (2, "transpose"), (3, "layer 3"), (4, "FPT step"), (5, "tick head"), (6, "planes"))
-            if os.environ.get("SGMM_FRONTIER_KERNEL") == "r4" else
-            ((1, "L1+L2 issue"), (2, "L2 drain+tr+L3"), (4, "FPT+stores"), (5, "tick head"), (6, "tick tail")))
-    if os.environ.get("SGMM_FRONTIER_KERNEL") != "r4":
+    labs = ((1, "L1+L2 issue"), (2, "L2 drain+tr+L3"), (4, "FPT+stores"), (5, "tick head"), (6, "tick tail"))
+    if True:
         print(f"  slots/wave {med(x[:, 3]):6.0f}  cycles per slot {med(x[:, 0] / np.maximum(x[:, 3], 1)):7.0f}"
               f"  (L1+L2 issue per slot {med(x[:, 1] / np.maximum(x[:, 3], 1)):6.0f}, drain+L3 per slot "
               f"{med(x[:, 2] / np.maximum(x[:, 3], 1)):6.0f}, FPT per slot {med(x[:, 4] / np.maximum(x[:, 3], 1)):6.0f})")

@@ -1,6 +1,6 @@
 # Round-5 A/B on one GPU box: alternate bench runs of variants given as
 # NAME=ENV_ASSIGNMENTS (space-separated, ';' for none), ROUNDS times each.
-# usage: bash tools/r05_ab.sh OUTDIR ROUNDS "bench args" "new=;" "r4=SGMM_FRONTIER_KERNEL=r4" ...
+# usage: bash tools/r05_ab.sh OUTDIR ROUNDS "bench args" "new=;" "head=SGMM_LIB=tools/variants/libsgmm_head.so" ...
 set -e
 out=$1; rounds=$2; args=$3; shift 3
 mkdir -p "$out"
