@@ -73,6 +73,9 @@ if os.environ.get("SCAN"):
           f"{np.median(tot):.0f} p90 {np.percentile(tot, 90):.0f} p99 {np.percentile(tot, 99):.0f} max {tot.max():.0f}; "
           f"span {(g_[:, 3].max() - g_[:, 0].min()):.0f}")
     ga, sm, it, fb = g_[:, 11], g_[:, 12], g_[:, 13], g_[:, 14]
+    pa, pb, wk = g_[:, 8] - g_[:, 2], g_[:, 9] - g_[:, 8], g_[:, 10] - g_[:, 9]
+    print(f"  the last window (med / p90 cycles): phase a {np.median(pa):.0f}/{np.percentile(pa, 90):.0f}, phase b "
+          f"{np.median(pb):.0f}/{np.percentile(pb, 90):.0f}, walk {np.median(wk):.0f}/{np.percentile(wk, 90):.0f}")
     print(f"  per episode: chunk starts med {np.median(g_[:, 1] - g_[:, 0]):.0f}, gather med {np.median(ga):.0f}, "
           f"exact sum med {np.median(sm):.0f}, walk iterations med {np.median(it):.0f}, fallback blocks med "
           f"{np.median(fb):.0f}")
