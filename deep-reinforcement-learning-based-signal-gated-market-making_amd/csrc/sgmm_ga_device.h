@@ -573,7 +573,24 @@ __device__ __forceinline__ void regen_master_wave(float* __restrict__ master, in
     }
 }
 
-template <bool HANDOFF>
+// master <- ask(best) by every thread of the workgroup (4 parameters a thread
+// at a time, each read before it is overwritten): the deferred half of the tell
+__device__ __forceinline__ void regen_master_block(float* __restrict__ master, int64_t n, float sig, uint64_t seed,
+                                                   uint32_t sid, uint32_t gen, int best) {
+    for (int64_t k4 = threadIdx.x; 4 * k4 < n; k4 += blockDim.x) {
+        float m[4], z[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = 4 * k4 + q < n ? master[4 * k4 + q] : 0.0f;
+        normal4(seed, sid, gen, (uint32_t)best, (uint32_t)k4, z);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * k4 + q < n) master[4 * k4 + q] = m[q] + z[q] * sig;  // ask_row4's arithmetic
+    }
+}
+
+// REGEN = false: the argmax and the bookkeeping only; master <- ask(best)
+// happens in the validation launch's tail (regen_master_block)
+template <bool HANDOFF, bool REGEN = true>
 __device__ void tell_wave(sgmm_ga_state* __restrict__ st, const double* __restrict__ fit,
                           const int32_t* __restrict__ trades, int32_t P, float* __restrict__ master,
                           float* __restrict__ master_adv, int64_t n_mm, int64_t n_adv, uint64_t seed,
@@ -615,8 +632,10 @@ __device__ void tell_wave(sgmm_ga_state* __restrict__ st, const double* __restri
     const double tf = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(bv), src));
     const int32_t ttr = __builtin_amdgcn_readlane(btr, src);
     // tell (model.py:73-76; drl_engine.py:119-125)
-    regen_master_wave(master, n_mm, sig_mm, seed, 0u, gen, best);
-    if (master_adv) regen_master_wave(master_adv, n_adv, sig_adv, seed, 1u, gen, abest);
+    if constexpr (REGEN) {
+        regen_master_wave(master, n_mm, sig_mm, seed, 0u, gen, best);
+        if (master_adv) regen_master_wave(master_adv, n_adv, sig_adv, seed, 1u, gen, abest);
+    }
     if (lane == 0) {
         st->best_idx = best;
         st->adv_best_idx = abest;

@@ -51,6 +51,9 @@ struct GenomeSrc {
     int32_t pop_eps;          // episodes per population (0: one population)
     const uint64_t* seeds;    // [K] per-population keys, or nullptr
     int64_t mm_pstride, adv_pstride;
+    // asked genomes: 1 = individual st->best_idx of the episode's population (the
+    // tell's argmax, its master update deferred to the validation launch's tail)
+    int32_t use_best = 0;
 };
 
 constexpr int kAdvParams = 74;  // AdversaryPolicy weights = first 74 floats of the genome
@@ -69,9 +72,10 @@ __device__ inline void stage_genomes(const GenomeSrc& src, int e, int gi, int ai
         const float* master = src.master_mm + (int64_t)k * src.mm_pstride;
         const uint32_t gen = (uint32_t)st->gen;
         const float sig = (float)st->sigma_mm;
+        const uint32_t ind = src.use_best ? (uint32_t)st->best_idx : (uint32_t)(src.i0 + gi);
         for (int k4 = tid; k4 < (n + 3) / 4; k4 += nt) {
             float v[4];
-            ask_row4(master, n, sig, seed, 0u, gen, (uint32_t)(src.i0 + gi), k4, v);
+            ask_row4(master, n, sig, seed, 0u, gen, ind, k4, v);
 #pragma unroll
             for (int q = 0; q < 4; ++q)
                 if (4 * k4 + q < n) gs[4 * k4 + q] = v[q];

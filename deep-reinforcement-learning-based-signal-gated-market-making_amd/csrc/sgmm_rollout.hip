@@ -1162,7 +1162,12 @@ struct StepArgs {
     // 0: the whole boundary (records: P training then P validation results per
     // population); 1: tell only (the validation of the new master follows in its
     // own launches); 2: validation bookkeeping, one episode per population
-    // (workgroup k = population k's post-tell master, validation_tail)
+    // (workgroup k = population k's post-tell master, validation_tail);
+    // 3: the tell's argmax only (the last arriver is a one-wave workgroup whose
+    // master regeneration took ~17 us, profiles/r05_timeline/sc_tr15d.txt) and
+    // 4: its validation launch -- episode k rolls out individual best of
+    // population k (GenomeSrc::use_best) and workgroup k regenerates the master
+    // (all its threads) before the bookkeeping
     int32_t mode;
 };
 
@@ -1214,7 +1219,11 @@ __device__ __forceinline__ void tail_run(const StepArgs& sa0, const double* fitn
     float* lm = reinterpret_cast<float*>(si + 2 * nt);
     float* la = lm + sa.n_mm;
     const bool tell_only = sa.mode == 1;
-    if (tell_only && nt == kWave && sa.n_mm <= 4 * kWave * kWaveChunks && sa.n_adv <= 4 * kWave * kWaveChunks)
+    if (sa.mode == 3) {
+        if (threadIdx.x < kWave)
+            tell_wave<true, false>(sa.st, fitness, trades, sa.P, sa.master_mm, sa.master_adv, sa.n_mm, sa.n_adv,
+                                   sa.seed, sa.history, sa.hist_cap);
+    } else if (tell_only && nt == kWave && sa.n_mm <= 4 * kWave * kWaveChunks && sa.n_adv <= 4 * kWave * kWaveChunks)
         tell_wave<true>(sa.st, fitness, trades, sa.P, sa.master_mm, sa.master_adv, sa.n_mm, sa.n_adv, sa.seed,
                         sa.history, sa.hist_cap);
     else if (sa.P <= nt && sa.n_mm <= 16 * nt && sa.n_adv <= 16 * nt)
@@ -1250,6 +1259,18 @@ __device__ __forceinline__ void generation_tail(const StepArgs& sa0, const doubl
 // master and runs its bookkeeping -- no other episode's record is needed.
 __device__ __forceinline__ void validation_tail(const StepArgs& sa, double v, int32_t vtr, int* flag, int k) {
     __syncthreads();  // flag aliases LDS the caller has just read
+    if (sa.mode == 4) {
+        // the deferred tell: master <- ask(best) with the generation's sigma and
+        // counter (the bookkeeping below decays sigma and advances gen)
+        const sgmm_ga_state* st = sa.st + k;
+        const uint32_t gen = (uint32_t)st->gen;
+        const int best = st->best_idx, abest = st->adv_best_idx;
+        const float smm = (float)st->sigma_mm, sadv = (float)st->sigma_adv;
+        const uint64_t seed = sa.seeds ? sa.seeds[k] : sa.seed;
+        regen_master_block(sa.master_mm + (int64_t)k * sa.n_mm, sa.n_mm, smm, seed, 0u, gen, best);
+        if (sa.master_adv) regen_master_block(sa.master_adv + (int64_t)k * sa.n_adv, sa.n_adv, sadv, seed, 1u, gen, abest);
+        __syncthreads();  // the new master before the checkpoint copy reads it
+    }
     val_update_dev(sa.st + k, v, vtr, sa.master_mm + (int64_t)k * sa.n_mm,
                    sa.best_master ? sa.best_master + (int64_t)k * sa.n_mm : nullptr, sa.n_mm,
                    sa.history ? sa.history + (int64_t)k * sa.hist_cap : nullptr, sa.hist_cap, flag);
@@ -1411,7 +1432,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
         store_record(fitness, trades_out, e, total, tr);
     }
     if (step.st) {
-        if (step.mode == 2) validation_tail(step, total, tr, sh.red, e);
+        if (step.mode == 2 || step.mode == 4) validation_tail(step, total, tr, sh.red, e);
         else generation_tail(step, fitness, trades_out, sh.tail, sh.red, e, n_total);
     }
 }
@@ -2137,7 +2158,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ep.gtail = plan.gtail;
         ep.whole = plan.whole;
     }
-    const bool vt = step.st && step.mode == 2;  // the validation launches (profiled separately)
+    const bool vt = step.st && (step.mode == 2 || step.mode == 4);  // the validation launches (profiled separately)
     SGMM_REQUIRE(fr || arl || eps->max_len <= kMaxLen,
                  "max_len=%d > %d needs the frontier kernel (hidden 16 or 32) or the adversary path", eps->max_len,
                  kMaxLen);
@@ -2300,16 +2321,28 @@ extern "C" int sgmm_generation_multi(const sgmm_ticks* ticks, const sgmm_episode
 // val_eps episode k runs masters_mm row val_eps->genome[k] (= k) with no
 // adversary; the scan's workgroup k then runs population k's validation
 // bookkeeping (validation_tail).  The policy kernel is the table (K episodes).
+// deferred: the training launch's tail ran the tell's argmax only (StepArgs
+// mode 3); episode k rolls out population k's best individual from the
+// pre-tell master and the scan's workgroup k writes the new master (mode 4)
 static int validate_impl(const sgmm_ticks* ticks, const sgmm_episodes* val_eps, const sgmm_env_params* params,
                          const sgmm_populations* pops, double* val_fitness, int32_t* val_trades, void* workspace,
-                         size_t workspace_bytes, hipStream_t s) {
+                         size_t workspace_bytes, hipStream_t s, bool deferred = false) {
     const int32_t H = pops->hidden, K = pops->n_pop;
     if (int rc = check_episodes(ticks, val_eps, params, pops->masters_mm, H)) return rc;
     SGMM_REQUIRE(val_eps->n == K, "validation episodes must be one per population (%d), got %d", K, val_eps->n);
     const int64_t n_mm = (int64_t)H * H + 7 * H + 2;
-    const GenomeSrc src{pops->masters_mm, n_mm, nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
-    StepArgs step{pops->states, pops->masters_mm, nullptr, pops->best_masters, n_mm, 0, 0,
-                  pops->history, pops->history_cap, 1, 1, pops->seeds, 2};
+    const bool arl = pops->masters_adv != nullptr;
+    GenomeSrc src{pops->masters_mm, n_mm, nullptr, 0, nullptr, nullptr, nullptr, 0, 0};
+    if (deferred) {
+        src = GenomeSrc{nullptr, 0, nullptr, 0, pops->states, pops->masters_mm, nullptr, 0, 0};
+        src.pop_eps = 1;
+        src.seeds = pops->seeds;
+        src.mm_pstride = n_mm;
+        src.use_best = 1;
+    }
+    StepArgs step{pops->states, pops->masters_mm, (deferred && arl) ? pops->masters_adv : nullptr, pops->best_masters,
+                  n_mm, (deferred && arl) ? (int64_t)kAdvGenome : 0, 0, pops->history, pops->history_cap, 1, 1,
+                  pops->seeds, deferred ? 4 : 2};
     return rollout_impl(ticks, val_eps, params, src, false, H, val_fitness, val_trades, workspace, workspace_bytes,
                         step, s);
 }
@@ -2347,12 +2380,12 @@ extern "C" int sgmm_generation_multi_best(const sgmm_ticks* ticks, const sgmm_ep
     src.mm_pstride = n_mm;
     src.adv_pstride = n_adv;
     StepArgs step{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, n_mm, n_adv, 0,
-                  pops->history, pops->history_cap, P, P, pops->seeds, 1};
+                  pops->history, pops->history_cap, P, P, pops->seeds, 3};
     hipStream_t s = as_stream(stream);
     if (int rc = rollout_impl(ticks, train_eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
                               step, s))
         return rc;
-    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s);
+    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s, true);
 }
 
 extern "C" int sgmm_rollout_fitness_asked_multi(const sgmm_ticks* ticks, const sgmm_episodes* eps,
