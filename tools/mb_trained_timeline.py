@@ -84,6 +84,12 @@ if os.environ.get("SCAN"):
     print(f"  blocks without a prediction per episode (med / p90): no binade {np.median(nf):.0f}/{np.percentile(nf, 90):.0f}, "
           f"bad step {np.median(nb):.0f}/{np.percentile(nb, 90):.0f}, binade edge {np.median(ne):.0f}/"
           f"{np.percentile(ne, 90):.0f}; zero blocks {np.median(g_[:, 7]):.0f}")
+    t4, t5 = g_[:, 4], g_[:, 5]
+    m_ = (t5 > t4) & (t4 > 0)
+    if m_.any():
+        print("  tell in the last arriver per population (e, cycles, end after the scan's first entry):",
+              [(int(e), int(t5[e] - t4[e]), int(t5[e] - g_[:, 0].min())) for e in np.where(m_)[0][:8]],
+              f"; the scan's last episode ends {int((g_[:, 3] * (g_[:, 3] > 0)).max() - g_[:, 0].min())}")
     o = np.argsort(tot)[::-1]
     print("  slowest (e, entry->end, gather, sum, iters, fallbacks):",
           [(int(e), int(tot[e]), int(ga[e]), int(sm[e]), int(it[e]), int(fb[e])) for e in o[:10]])
