@@ -701,6 +701,140 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
 #endif
 }
 
+// ------------------------------------------------------------------ table, one state per wave (small launches)
+// The v3 table's arithmetic with its state loop spread over the workgroup: one
+// workgroup per 64-tick chunk, wave si runs layers 1-3 and the FPT step from
+// inventory state si, and wave 0 assembles the chunk's map, path planes and
+// trade counts from the states' successor bytes and rewards in LDS.  For
+// launches with few chunks (the validation rollouts: 5 x 15 chunks at config
+// 3) the v3 wave's serial five-state chain is the launch's latency; here it is
+// one state deep.  Outputs are identical to v3's (same per-tick arithmetic).
+template <int H, int NSI>
+__global__ __launch_bounds__(kWave * NSI) void k_policy_table_sp(
+    sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
+    int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
+    double* __restrict__ rew) {
+    static_assert(H % 16 == 0 && H <= 32, "state-parallel table: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16, KS = H / 4, HP = H + 4;
+    const int e = blockIdx.y;
+    const int32_t T = ep.len[e];
+    const int chunk = blockIdx.x;
+    const int32_t t0 = chunk * kChunk;
+    if (t0 >= T) return;  // block-uniform
+    const int si = threadIdx.x >> 6;  // this wave's inventory state (blockDim = 64 nsi)
+    const int lane = threadIdx.x & (kWave - 1), grp = lane >> 4, col = lane & 15;
+    const int64_t tb = ep.tick_off[e];
+    float xs0[4], xs1[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int64_t ti = tb + min(t0 + 16 * q + col, T - 1);
+        xs0[q] = tk.s1n[ti];
+        xs1[q] = tk.s2n[ti];
+    }
+    const int64_t tix = tb + min(t0 + lane, T - 1);
+    const double tmid = tk.mid_next[tix], task = tk.best_ask[tix], tbid = tk.best_bid[tix];
+    const double tbmax = tk.buy_max[tix], tsmin = tk.sell_min[tix];
+    __shared__ __attribute__((aligned(16))) float gsm[L::N];
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H];
+    __shared__ __attribute__((aligned(16))) float hb_s[NSI][kWave * HP];
+    __shared__ __attribute__((aligned(16))) double rl_s[NSI][kWave];  // [state][lane] rewards
+    __shared__ uint8_t to_s[NSI][kWave];  // successor state | traded << 7
+    stage_genomes(src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+    __syncthreads();
+    if (threadIdx.x < 2 * H) w3i[threadIdx.x] = gsm[L::W3 + (threadIdx.x & 1) * H + (threadIdx.x >> 1)];
+    const float* g = gsm;
+    float w2f[NT][KS];
+    f32x4 b2c[NT];
+#pragma unroll
+    for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+        for (int i = 0; i < KS; ++i) w2f[rt][i] = g[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b2c[rt][r] = g[L::B2 + 16 * rt + 4 * grp + r];
+    }
+    const float x2 = (float)((double)(inv_min + si) / 2.0);
+    float h1[KS][4];
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const int k = 4 * i + grp;
+        const float a0 = g[L::W1 + 3 * k], a1 = g[L::W1 + 3 * k + 1], bb = g[L::B1 + k], w1s = g[L::W1 + 3 * k + 2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            h1[i][q] = relu(__builtin_fmaf(w1s, x2, __builtin_fmaf(a1, xs1[q], __builtin_fmaf(a0, xs0[q], bb))));
+    }
+    const float b30 = g[L::B3], b31 = g[L::B3 + 1];
+    __syncthreads();  // w3i complete
+    const sgmm_env_params p = params[ep.param[e]];
+    float* hb = hb_s[si];
+    f32x4 acc[4][NT];
+#pragma unroll
+    for (int i = 0; i < KS; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int rt = 0; rt < NT; ++rt)
+                acc[q][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[i][q], i == 0 ? b2c[rt] : acc[q][rt],
+                                                                  0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int rt = 0; rt < NT; ++rt) {
+            f32x4 v;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = relu(acc[q][rt][r]);
+            *reinterpret_cast<f32x4*>(&hb[(16 * q + col) * HP + 16 * rt + 4 * grp]) = v;
+        }
+    float o0 = b30, o1 = b31;
+#pragma unroll
+    for (int j4 = 0; j4 < H / 4; ++j4) {
+        const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+        for (int r2 = 0; r2 < 2; ++r2) {
+            const f32x4 w = *reinterpret_cast<const f32x4*>(&w3i[2 * (4 * j4 + 2 * r2)]);
+            o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+            o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+            o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+            o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+        }
+    }
+    const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+    const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+    const StepOut so = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
+    to_s[si][lane] = (uint8_t)((si + so.fill_buy - so.fill_sell) | ((so.fill_buy | so.fill_sell) << 7));
+    rl_s[si][lane] = so.reward;
+    __syncthreads();
+    if (si != 0) return;
+    // wave 0: the chunk's map, path planes and trade counts (v3's tail)
+    const bool valid = t0 + lane < T;
+    uint64_t map = kIdentityMap;
+    uint32_t traded = 0;
+    if (valid) {
+        for (int s = 0; s < nsi; ++s) {
+            const uint32_t b = to_s[s][lane];
+            map = (map & ~(0xFFull << (8 * s))) | ((uint64_t)(b & 0x7Fu) << (8 * s));
+            traded |= (b >> 7) << s;
+        }
+    }
+    const uint64_t inc = wave_map_scan(map);
+    uint64_t excl = shfl_up_u64(inc, 1);
+    if (lane == 0) excl = kIdentityMap;
+    const int64_t row = ep.step_off[e] + t0 + lane;
+    uint64_t cnt = 0;
+#pragma unroll
+    for (int s0 = 0; s0 < NSI; ++s0) {
+        if (s0 >= nsi) break;
+        const uint32_t st = map_get(excl, (uint32_t)s0);
+        if (valid) rew[s0 * ep.rs + row] = rl_s[st][lane];
+        cnt |= (uint64_t)__popcll(__ballot(valid && ((traded >> st) & 1u))) << (8 * s0);
+    }
+    if (lane == kWave - 1) {
+        const uint32_t ci = chunk_base(ep.step_off[e], e) + chunk;
+        cmaps[ci] = inc;
+        ctr[ci] = cnt;
+    }
+}
+
 
 // ------------------------------------------------------------------ exact ordered sum
 // The episode total is the reference's sequential float64 sum
@@ -2028,6 +2162,14 @@ static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     return eps->n >= min_eps;
 }
 
+// The one-state-per-wave table for launches of at most kTableSpChunks chunks
+// (SGMM_TABLE_SP=0 / 1 forces v3 / it, for A/B and the tests)
+constexpr int64_t kTableSpChunks = 256;
+static bool table_sp(int nch, int n_ep) {
+    if (const char* v = std::getenv("SGMM_TABLE_SP")) return std::atoi(v) != 0;
+    return (int64_t)nch * n_ep <= kTableSpChunks;
+}
+
 template <int H>
 static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
                               const sgmm_ticks& tk, const EpArrays& ep,
@@ -2036,6 +2178,16 @@ static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStrea
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
     if constexpr (H <= 32) {
+        if (!arl && table_sp(nch, n_ep)) {
+            const dim3 g2(nch, n_ep), b2(kWave * nsi);  // one workgroup per chunk, one wave per state
+            if (nsi <= 5)
+                SGMM_LAUNCH((k_policy_table_sp<H, 5>), g2, b2, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
+                            rew);
+            else
+                SGMM_LAUNCH((k_policy_table_sp<H, 8>), g2, b2, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
+                            rew);
+            return;
+        }
         if (!arl) {
             if (nsi <= 5)
                 SGMM_LAUNCH((k_policy_table_v3<H, 5>), grid, block, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,

@@ -285,12 +285,16 @@ def test_scan_ragged_lengths(golden, sgmm, oracle):
             assert trd[i].item() == t and fit[i].item() == f, (H, i)
 
 
-@pytest.mark.parametrize("path", ["valu", "table", "frontier"])
+@pytest.mark.parametrize("path", ["valu", "table", "table_v3", "frontier"])
 def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
-    """Every policy kernel -- the VALU table, the f32-MFMA table (v3 schedule;
+    """Every policy kernel -- the VALU table, the f32-MFMA tables (one state per
+    wave for small launches, the v3 schedule forced by SGMM_TABLE_SP=0;
     k_policy_table_mfma with the adversary and for H = 64) and the frontier
     kernel -- reproduces the oracle's canonical fma chains bit for bit (the MFMA
     k-order equals the chain)."""
+    if path == "table_v3":
+        monkeypatch.setenv("SGMM_TABLE_SP", "0")
+        path = "table"
     monkeypatch.setenv("SGMM_TABLE_PATH", path)
     eps = list(episodes_from_fixture(golden("g2_synthetic.npz")))
     eps += _synthetic_batch(sgmm, 4, 1000, 32, seed=77, sigma=0.4)
@@ -299,6 +303,42 @@ def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
         for i, ep in enumerate(group):
             f, t = _oracle_eval(oracle, ep)
             assert trd[i].item() == t and fit[i].item() == f, (path, H, arl, i)
+
+
+@pytest.mark.parametrize("caps", [(0, 0), (1, -1), (2, -2), (3, -4)], ids=["nsi1", "nsi3", "nsi5", "nsi8"])
+@pytest.mark.parametrize("H", [16, 32])
+def test_state_parallel_table(sgmm, oracle, caps, H, monkeypatch):
+    """The one-state-per-wave table (k_policy_table_sp, launches of at most 256
+    chunks) and the v3 table agree bit for bit with each other and the oracle,
+    for 1, 3, 5 and 8 inventory states and ragged lengths (partial last chunk,
+    zero-length and one-tick episodes)."""
+    from sgmm_amd import synthetic
+    i_max, i_min = caps
+    lens = np.array([0, 1, 63, 64, 65, 700, 912, 1000], np.int64)
+    P, T = len(lens), int(lens.max())
+    b = synthetic.bundle_510300(T, seed=5)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=0.3, seed=6)
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0001, tick_size=0.001, i_max=i_max, i_min=i_min)], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
+                           inv_min=i_min, inv_max=i_max).to(DEV)
+    monkeypatch.setenv("SGMM_TABLE_PATH", "table")
+    got = {}
+    for sp in ("1", "0"):
+        monkeypatch.setenv("SGMM_TABLE_SP", sp)
+        fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
+        got[sp] = (fit.cpu().numpy(), trd.cpu().numpy())
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,
+                                           np.zeros(P), lens, np.zeros(P),
+                                           [oracle.params(phi=0.0001, tick=0.001, i_max=i_max, i_min=i_min)],
+                                           n_threads=8)
+    for sp, (f, t) in got.items():
+        assert np.array_equal(t, want_t), sp
+        assert np.array_equal(f, want_f), sp
 
 
 def _seq_sum(init, x):

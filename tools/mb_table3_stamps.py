@@ -17,7 +17,7 @@ sg = sgmm_pkg.load()
 from sgmm_amd import _lib, synthetic
 L = _lib.load()
 L.sgmm_debug_tstamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-T, H = 4560, int(os.environ.get("H", 32))
+T, H = int(os.environ.get("T", 4560)), int(os.environ.get("H", 32))
 dev = torch.device("cuda")
 b = synthetic.bundle_510300(T, seed=0)
 st = synthetic.train_stats(b)

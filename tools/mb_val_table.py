@@ -1,6 +1,6 @@
 """Diagnostic: the validation launch's shape (K episodes of T ticks, H=32) on the
-table paths -- v3 (MFMA, one wave per 64-tick chunk, the five states in turn)
-and the VALU table (one wave per (chunk, state)) -- kernel times by HIP events.
+table paths -- the one-state-per-wave MFMA table (default for small launches),
+v3 (MFMA, one wave per 64-tick chunk, the five states in turn) and the VALU table (one wave per (chunk, state)) -- kernel times by HIP events.
     python tools/mb_val_table.py [K=5] [T=912]"""
 import os
 import sys
@@ -23,8 +23,9 @@ params = sg.params_tensor([sg.EnvConfig(phi=1e-4, tick_size=0.001)], dev)
 pop = synthetic.population(K, H, sigma=0.1, seed=4).to(dev)
 eb = sg.EpisodeBatch(np.arange(K), np.zeros(K), np.full(K, T), np.zeros(K)).to(dev)
 out = {}
-for path in ("table", "valu"):
-    os.environ["SGMM_TABLE_PATH"] = path
+for path in ("table", "v3", "valu"):
+    os.environ["SGMM_TABLE_PATH"] = "table" if path == "v3" else path
+    os.environ["SGMM_TABLE_SP"] = "0" if path == "v3" else "1"
     eng = sg.RolloutEngine(dev)
     for _ in range(5):
         f, t = eng.fitness(ticks, eb, params, pop, H)
@@ -38,5 +39,6 @@ for path in ("table", "valu"):
     _lib.profile_enable(False)
     out[path] = (f.cpu().numpy(), t.cpu().numpy())
     print(path, {k: round(v[0] * 1e3 / v[1], 2) for k, v in prof.items()}, "us per launch")
-assert np.array_equal(out["table"][0], out["valu"][0]) and np.array_equal(out["table"][1], out["valu"][1])
+for k in ("v3", "valu"):
+    assert np.array_equal(out["table"][0], out[k][0]) and np.array_equal(out["table"][1], out[k][1])
 print("fitness identical")
