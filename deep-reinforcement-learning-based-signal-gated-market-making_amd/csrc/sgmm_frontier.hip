@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     // the tick's extra (chunk, state) pairs: lane << 3 | state, then the
     // successor (bits 9-11) and the fill (bit 12) written back by the column
     __shared__ uint16_t pl[kWave * (NSI - 1)];
+    __shared__ uint32_t nslot_s;  // MLP slots run (FrontierArgs::wslots; in LDS: the walk loop has no register to spare)
 
     const sgmm_ticks& tk = args.tk;
     const EpArrays& ep = args.ep;
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
     int fr_extra = 0;
+    if (LS == 1 && lane == 0) nslot_s = 0;
 
     // layers 1-3 for the columns of this slot (their inputs in the rows of
     // hb as (s1, s2, inv/2, 0)); tiles >= NQ are skipped; o0 / o1 = the
@@ -314,6 +316,8 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         // apart: a heavy walk, the launch's tail) takes the SIMD's issue
         // priority over the light walks beside it (round 4, profiles/r04_ab)
         fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
+        if (LS == 1 && lane == 0)  // (the walk-order feedback is for one wave per walk)
+            __hip_atomic_fetch_add(&nslot_s, (uint32_t)((any0 ? 1 : 0) + nx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         if ((tt & 7) == 7) {
             if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
             else __builtin_amdgcn_s_setprio(0);
@@ -511,6 +515,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 #pragma unroll
         for (int s = 0; s < NSI; ++s) ctr32[ci * 8 + s] = ((cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu) + (((sset >> s) & 1u) ? mcnt : 0u);
         kinfo[ci] = (uint32_t)kc | ((uint32_t)nw << 20) | (p0 << 29);
+        // the walk's slot count at (its first record) / 64 = e * ngrp + cg: indexed from
+        // the live record index (a block index kept to here costs spills)
+        if (LS == 1 && lane == 0 && args.wslots)
+            args.wslots[ci / NL] = __hip_atomic_load(&nslot_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
 }
 

@@ -222,6 +222,7 @@ struct FrontierArgs {
     uint32_t* ctr32;
     uint32_t* kinfo;
     double* rew;
+    uint32_t* wslots;  // one wave per walk: [e * ngrp + cg] = the MLP slots it ran (walk-order feedback), or null
 };
 
 // launches the frontier kernel for hidden = 16 / 32 and nsi inventory states

@@ -2092,7 +2092,7 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
 //   no adversary: u64 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
-//                 slots) | u32 kinfo[n * 64 G] | f64 path planes
+//                 slots) | u32 kinfo[n * 64 G] | u32 wslots[n * 64] | f64 path planes
 //                 rew[n_states][rs] (rs = total_steps + frontier_pad(G) n,
 //                 rounded up to 32; G = frontier_groups(n))
 //   adversary:    u64 fills[total_steps] | f64 rew[n_states][rs] (rs =
@@ -2111,6 +2111,8 @@ static size_t ws_ctr(int32_t n, int64_t steps) {
 // u32 kinfo[n * 256]: per chunk record the merge tick | p0 << 29
 static size_t ws_kinfo(int32_t n) { return align256(n_frontier_slots(n) * sizeof(uint32_t)); }
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
+// u32 wslots[n * 64]: the frontier launch's MLP slots per walk, [e * G + group] (G <= 16)
+static size_t ws_wslots(int32_t n) { return align256((size_t)n * 64 * sizeof(uint32_t)); }
 
 // The workspace of a batch with n_inventory inventory values, with or
 // without the adversary (then 4 * n_inventory states: inventory x previous
@@ -2121,7 +2123,7 @@ static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t 
     if (arl)  // fill codes, per-state planes rew[state * rs + row]
         return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes, true) * (size_t)(4 * nsi) * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
+           ws_wslots(n_episodes) + (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
 }
 
 extern "C" size_t sgmm_rollout_workspace_bytes(int32_t n_episodes, int64_t total_steps, int32_t n_inventory,
@@ -2271,6 +2273,66 @@ static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const
                     rew, fitness, trades, step);
 }
 
+// ------------------------------------------------------------------ walk order feedback
+// A launch with whole walks and walks in halves (frontier_plan's four-walk
+// rule, config 3: 1 024 whole + 1 536 in halves) ends with its heaviest whole
+// walk: the walks of a GA-trained population differ in how long their paths
+// stay apart, and the populations differ in how heavy their tails are
+// (config 3 after 15 generations: the heaviest whole walk of population 0 ran
+// 167 slots / 557 us, population 1's 116; every half walk ended by 430 us;
+// profiles/r05_timeline/tlo_*).  After each training launch of
+// sgmm_generation_multi_best this kernel ranks the populations by the heaviest
+// episode they just ran -- a whole walk's slots x 5, an episode in halves the
+// sum of its halves' slots x 4 (the halves' extra chunk starts: ~25 % more
+// slots for the same episode) -- and rewrites the order so the next launch
+// walks the lightest populations whole and cuts the heaviest into halves.
+// Scheduling only: every result is per episode and independent of the order.
+// (SGMM_FRONTIER_REORDER=0 keeps the caller's order.)
+constexpr int kReorderMaxPops = 64;
+__global__ __launch_bounds__(kScanThreads) void k_walk_reorder(const uint32_t* __restrict__ wslots,
+                                                               int32_t* __restrict__ order, int32_t n, int32_t whole,
+                                                               int32_t gtail, int32_t pop_eps) {
+    __shared__ uint32_t score[kReorderMaxPops];
+    __shared__ int32_t rank[kReorderMaxPops];
+    const int npop = n / pop_eps;
+    if ((int)threadIdx.x < npop) score[threadIdx.x] = 0;
+    __syncthreads();
+    for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
+        const int e = order[pos];  // its walks' slots at wslots[e * gtail + g] (gtail = the record layout's groups)
+        uint32_t sc;
+        if (pos < whole) {
+            sc = 5u * wslots[e * gtail];
+        } else {
+            uint32_t sum = 0;
+            for (int g = 0; g < gtail; ++g) sum += wslots[e * gtail + g];
+            sc = 4u * sum;
+        }
+        atomicMax(&score[e / pop_eps], sc);
+    }
+    __syncthreads();  // every read of the old order precedes the writes below
+    if (threadIdx.x == 0) {  // populations by (score, index), lightest first
+        for (int k = 0; k < npop; ++k) rank[k] = k;
+        for (int i = 1; i < npop; ++i)
+            for (int j = i; j > 0 && score[rank[j]] < score[rank[j - 1]]; --j) {
+                const int t = rank[j];
+                rank[j] = rank[j - 1];
+                rank[j - 1] = t;
+            }
+    }
+    __syncthreads();
+    for (int pos = threadIdx.x; pos < n; pos += blockDim.x) order[pos] = rank[pos / pop_eps] * pop_eps + pos % pop_eps;
+}
+// the launches the feedback applies to: a mixed whole / halves plan of one wave
+// per walk, whole populations of equal-length episodes, a caller's order array
+static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, const GenomeSrc& src) {
+    const char* v = std::getenv("SGMM_FRONTIER_REORDER");
+    const bool on = !(v && std::strcmp(v, "0") == 0);
+    const int P = src.pop_eps;
+    return on && eps->order && P > 0 && eps->n % P == 0 && eps->n / P >= 2 && eps->n / P <= kReorderMaxPops &&
+           plan.ls == 1 && plan.g0 == 1 && plan.gtail == 2 && plan.whole > 0 && plan.whole < eps->n &&
+           eps->total_steps == (int64_t)eps->n * eps->max_len;
+}
+
 // table + path scan (+ the generation tail when step.st) for one batch
 static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                         const sgmm_env_params* params, const GenomeSrc& src, bool arl,
@@ -2290,6 +2352,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     uint64_t* cmaps = nullptr;
     uint64_t* fills = nullptr;
     uint32_t* kinfo = nullptr;
+    uint32_t* wslots = nullptr;
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
@@ -2299,7 +2362,8 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         cmaps = reinterpret_cast<uint64_t*>(w);
         ctr = reinterpret_cast<uint64_t*>(w + a);
         kinfo = reinterpret_cast<uint32_t*>(w + a + b);
-        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n));
+        wslots = reinterpret_cast<uint32_t*>(w + a + b + ws_kinfo(eps->n));
+        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n));
     }
     EpArrays ep = ep_arrays(eps, arl);
     const bool fr = use_frontier(arl, hidden, eps);
@@ -2319,7 +2383,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     if (fr && eps->max_len > 0) {
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
         const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
-                              kinfo, rew};
+                              kinfo, rew, wslots};
         if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, plan.ls, s, fa)) return rc;
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
@@ -2381,6 +2445,11 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         }
     }
     SGMM_LAUNCHED();
+    if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src)) {
+        SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, wslots, const_cast<int32_t*>(eps->order), eps->n,
+                    plan.whole, plan.gtail, src.pop_eps);
+        SGMM_LAUNCHED();
+    }
     return SGMM_OK;
 }
 

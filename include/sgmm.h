@@ -342,7 +342,12 @@ int sgmm_rollout_fitness_asked_multi(const sgmm_ticks *ticks, const sgmm_episode
  * fitness/trades [K*P] (training), val_fitness/val_trades [K].  The workspace
  * must hold the larger of the two batches: sgmm_rollout_workspace_bytes(n,
  * steps, n_inventory, with_adversary) of each, with_adversary = masters_adv !=
- * NULL for the training batch and 0 for the validation batch. */
+ * NULL for the training batch and 0 for the validation batch.  When the
+ * frontier kernel cuts some training episodes into halves (2.5-4 episodes per
+ * SIMD) and the populations' episodes are of equal length, train_eps->order is
+ * rewritten on the device after the training launch so the next generation
+ * walks the lightest populations whole (scheduling only: results do not depend
+ * on the order; SGMM_FRONTIER_REORDER=0 disables it). */
 int sgmm_generation_multi_best(const sgmm_ticks *ticks, const sgmm_episodes *train_eps,
                                const sgmm_episodes *val_eps, const sgmm_env_params *params,
                                const sgmm_populations *pops, double *fitness, int32_t *trades,

@@ -70,9 +70,9 @@ def test_argument_errors_need_no_gpu(sgmm):
     # frontier kernel (64 G chunk records per episode -- G = 8 groups of 64 chunks at 4
     # episodes, the default rule's cap: u64 map, u32[8] counts, u32 merge info) (planes:
     # 1000 ticks + 4 x (256 G + 16) padding rows of the frontier layout -- 128-byte aligned
-    # episode blocks -- rounded to 32: 9280)
+    # episode blocks -- rounded to 32: 9280); u32 slots per frontier wave (64 per episode)
     assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 512 * 8 + 4 * 512 * 32 + 4 * 512 * 4
-                                                         + 5 * 9280 * 8)
+                                                         + 4 * 64 * 4 + 5 * 9280 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)

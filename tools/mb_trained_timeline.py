@@ -56,7 +56,11 @@ ticks = sg.TickStore()
 seg = ticks.segments[ticks.add(tr[0], st[0])]
 ticks.to(DEV)
 n = K * P
-eps = sg.EpisodeBatch(np.arange(n), np.full(n, seg[0]), np.full(n, T), np.repeat(np.arange(K), P)).to(DEV)
+eps = sg.EpisodeBatch(np.arange(n), np.full(n, seg[0]), np.full(n, T), np.repeat(np.arange(K), P))
+if os.environ.get("ORDER"):  # population order of the walks (the first ones are whole walks), e.g. ORDER=1,4,0,2,3
+    eps.order = np.concatenate([np.arange(k * P, (k + 1) * P) for k in map(int, os.environ["ORDER"].split(","))]
+                               ).astype(np.int32)
+eps = eps.to(DEV)
 params = sg.params_tensor([sg.EnvConfig(phi=phi, tick_size=tick) for phi, tick, _ in spec["pops"]], DEV)
 eng2 = sg.RolloutEngine(DEV)
 for _ in range(3):
@@ -178,3 +182,15 @@ for name, pr in (("s8", s8), ("s16", s16)):
         sel = x >= thr
         print(f"    {name} >= {thr:.0f}: selects {sel.sum()} walks, catches {np.sum(sel & top)} of {top.sum()} top-5%;"
               f" their total slots med {np.median(y[sel]):.0f}")
+# per population (episode e belongs to population e // P): the walks' slots and durations,
+# and the episodes' total slots over their chunk groups
+ep_of = rows % 16384
+grp_of = rows // 16384
+ep_slots = np.bincount(ep_of, weights=sl, minlength=K * P)
+for k in range(K):
+    m = (ep_of // P) == k
+    es = ep_slots[k * P:(k + 1) * P]
+    print(f"  population {k}: walks {m.sum()} (groups {sorted(set(grp_of[m].tolist()))}); walk slots med "
+          f"{np.median(sl[m]):.0f} p99 {np.percentile(sl[m], 99):.0f}; walk duration med {np.median(dur[m]) / 1e3:.1f} "
+          f"p99 {np.percentile(dur[m], 99) / 1e3:.1f} max {dur[m].max() / 1e3:.1f} us; episode slots med "
+          f"{np.median(es):.0f} p99 {np.percentile(es, 99):.0f} max {es.max():.0f}")
