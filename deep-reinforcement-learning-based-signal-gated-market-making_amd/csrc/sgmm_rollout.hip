@@ -701,6 +701,94 @@ __global__ __launch_bounds__(kWave * 4, H <= 16 ? (NSI <= 5 ? 5 : 4) : 2) void k
 #endif
 }
 
+// ------------------------------------------------------------------ walk order feedback
+// A launch with whole walks and walks in halves (frontier_plan's four-walk
+// rule, config 3: 1 024 whole + 1 536 in halves) ends with its heaviest whole
+// walk: the walks of a GA-trained population differ in how long their paths
+// stay apart, and the populations differ in how heavy their tails are
+// (config 3 after 15 generations: the heaviest whole walk of population 0 ran
+// 167 slots / 557 us, population 1's 116; every half walk ended by 430 us;
+// profiles/r05_timeline/tlo_*).  After each training launch of
+// sgmm_generation_multi_best this kernel ranks the populations by the heaviest
+// episode they just ran -- a whole walk's slots x 5, an episode in halves the
+// sum of its halves' slots x 4 (the halves' extra chunk starts: ~25 % more
+// slots for the same episode) -- and rewrites the order so the next launch
+// walks the lightest populations whole and cuts the heaviest into halves.
+// Scheduling only: every result is per episode and independent of the order.
+// (SGMM_FRONTIER_REORDER=0 keeps the caller's order.)
+// The job rides along as one extra workgroup of the validation table launch
+// that follows (k_policy_table_sp), which hides its ~6 us of latency; alone
+// (k_walk_reorder) where that launch takes another path.
+constexpr int kReorderMaxPops = 64;
+struct ReorderJob {
+    const uint32_t* wslots;
+    int32_t* order;  // null: no job
+    int32_t n, whole, gtail, pop_eps;
+};
+__device__ __forceinline__ void walk_reorder_block(const ReorderJob rj) {
+    const uint32_t* __restrict__ wslots = rj.wslots;
+    int32_t* __restrict__ order = rj.order;
+    const int32_t n = rj.n, whole = rj.whole, gtail = rj.gtail, pop_eps = rj.pop_eps;
+    const int nt = (int)blockDim.x;
+    __shared__ uint32_t score[kReorderMaxPops];
+    __shared__ int32_t rank[kReorderMaxPops];
+    const int npop = n / pop_eps;
+    if ((int)threadIdx.x < npop) score[threadIdx.x] = 0;
+    __syncthreads();
+    // four positions per thread in flight: the order loads, then the slot loads (two
+    // dependent load rounds per 4 096 positions instead of two per 1 024)
+    constexpr int kPer = 4;
+    for (int base = 0; base < n; base += nt * kPer) {
+        int e[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int pos = base + j * nt + (int)threadIdx.x;
+            e[j] = pos < n ? order[pos] : -1;
+        }
+        uint32_t sc[kPer];
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {  // the episode's walks' slots at wslots[e * gtail + g]
+            const int pos = base + j * nt + (int)threadIdx.x;
+            sc[j] = 0;
+            if (e[j] < 0) continue;
+            if (pos < whole) {
+                sc[j] = 5u * wslots[e[j] * gtail];
+            } else {
+                uint32_t sum = 0;
+                for (int g = 0; g < gtail; ++g) sum += wslots[e[j] * gtail + g];
+                sc[j] = 4u * sum;
+            }
+        }
+        // one LDS atomic per wave where its 64 positions are one population (the usual
+        // case: the order is population blocks), per lane otherwise
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int k = e[j] < 0 ? -1 : e[j] / pop_eps;
+            const int k0 = __builtin_amdgcn_readfirstlane(k);
+            if (__all(k == k0)) {
+                uint32_t m = sc[j];
+#pragma unroll
+                for (int d = 1; d < kWave; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, kWave));
+                if ((threadIdx.x & (kWave - 1)) == 0 && k0 >= 0) atomicMax(&score[k0], m);
+            } else if (k >= 0) {
+                atomicMax(&score[k], sc[j]);
+            }
+        }
+    }
+    __syncthreads();  // every read of the old order precedes the writes below
+    if (threadIdx.x == 0) {  // populations by (score, index), lightest first
+        for (int k = 0; k < npop; ++k) rank[k] = k;
+        for (int i = 1; i < npop; ++i)
+            for (int j = i; j > 0 && score[rank[j]] < score[rank[j - 1]]; --j) {
+                const int t = rank[j];
+                rank[j] = rank[j - 1];
+                rank[j - 1] = t;
+            }
+    }
+    __syncthreads();
+    for (int pos = threadIdx.x; pos < n; pos += blockDim.x) order[pos] = rank[pos / pop_eps] * pop_eps + pos % pop_eps;
+}
+__global__ __launch_bounds__(1024) void k_walk_reorder(ReorderJob rj) { walk_reorder_block(rj); }
 // ------------------------------------------------------------------ table, one state per wave (small launches)
 // The v3 table's arithmetic with its state loop spread over the workgroup: one
 // workgroup per 64-tick chunk, wave si runs layers 1-3 and the FPT step from
@@ -713,10 +801,14 @@ template <int H, int NSI>
 __global__ __launch_bounds__(kWave * NSI) void k_policy_table_sp(
     sgmm_ticks tk, EpArrays ep, const sgmm_env_params* __restrict__ params, GenomeSrc src,
     int32_t inv_min, int32_t nsi, uint64_t* __restrict__ ctr, uint64_t* __restrict__ cmaps,
-    double* __restrict__ rew) {
+    double* __restrict__ rew, ReorderJob rj) {
     static_assert(H % 16 == 0 && H <= 32, "state-parallel table: H = 16 or 32");
     using L = GenomeLayout<H>;
     constexpr int NT = H / 16, KS = H / 4, HP = H + 4;
+    if (rj.order && blockIdx.y == gridDim.y - 1) {  // the extra workgroup: the walk-order job
+        if (blockIdx.x == 0) walk_reorder_block(rj);
+        return;
+    }
     const int e = blockIdx.y;
     const int32_t T = ep.len[e];
     const int chunk = blockIdx.x;
@@ -2172,22 +2264,27 @@ static bool table_sp(int nch, int n_ep) {
     return (int64_t)nch * n_ep <= kTableSpChunks;
 }
 
+// rj (may be null): a walk-order job to run as the state-parallel table's extra
+// workgroup; *rj_done tells whether it did
 template <int H>
 static void launch_table_mfma(bool arl, int nsi, int max_len, int n_ep, hipStream_t s,
                               const sgmm_ticks& tk, const EpArrays& ep,
                               const sgmm_env_params* params, const GenomeSrc& src, int32_t inv_min,
-                              uint64_t* ctr, uint64_t* cmaps, uint64_t* fills, double* rew) {
+                              uint64_t* ctr, uint64_t* cmaps, uint64_t* fills, double* rew,
+                              const ReorderJob* rj = nullptr, bool* rj_done = nullptr) {
     const int nch = (max_len + kChunk - 1) / kChunk;
     const dim3 grid((nch + 3) / 4, n_ep), block(kWave * 4);  // 4 chunks (waves) per block
     if constexpr (H <= 32) {
         if (!arl && table_sp(nch, n_ep)) {
-            const dim3 g2(nch, n_ep), b2(kWave * nsi);  // one workgroup per chunk, one wave per state
+            const ReorderJob job = rj ? *rj : ReorderJob{nullptr, nullptr, 0, 0, 0, 1};
+            const dim3 g2(nch, n_ep + (job.order ? 1 : 0)), b2(kWave * nsi);  // one workgroup per chunk, one wave per state
             if (nsi <= 5)
                 SGMM_LAUNCH((k_policy_table_sp<H, 5>), g2, b2, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
-                            rew);
+                            rew, job);
             else
                 SGMM_LAUNCH((k_policy_table_sp<H, 8>), g2, b2, 0, s, tk, ep, params, src, inv_min, nsi, ctr, cmaps,
-                            rew);
+                            rew, job);
+            if (rj_done) *rj_done = job.order != nullptr;
             return;
         }
         if (!arl) {
@@ -2273,55 +2370,6 @@ static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const
                     rew, fitness, trades, step);
 }
 
-// ------------------------------------------------------------------ walk order feedback
-// A launch with whole walks and walks in halves (frontier_plan's four-walk
-// rule, config 3: 1 024 whole + 1 536 in halves) ends with its heaviest whole
-// walk: the walks of a GA-trained population differ in how long their paths
-// stay apart, and the populations differ in how heavy their tails are
-// (config 3 after 15 generations: the heaviest whole walk of population 0 ran
-// 167 slots / 557 us, population 1's 116; every half walk ended by 430 us;
-// profiles/r05_timeline/tlo_*).  After each training launch of
-// sgmm_generation_multi_best this kernel ranks the populations by the heaviest
-// episode they just ran -- a whole walk's slots x 5, an episode in halves the
-// sum of its halves' slots x 4 (the halves' extra chunk starts: ~25 % more
-// slots for the same episode) -- and rewrites the order so the next launch
-// walks the lightest populations whole and cuts the heaviest into halves.
-// Scheduling only: every result is per episode and independent of the order.
-// (SGMM_FRONTIER_REORDER=0 keeps the caller's order.)
-constexpr int kReorderMaxPops = 64;
-__global__ __launch_bounds__(kScanThreads) void k_walk_reorder(const uint32_t* __restrict__ wslots,
-                                                               int32_t* __restrict__ order, int32_t n, int32_t whole,
-                                                               int32_t gtail, int32_t pop_eps) {
-    __shared__ uint32_t score[kReorderMaxPops];
-    __shared__ int32_t rank[kReorderMaxPops];
-    const int npop = n / pop_eps;
-    if ((int)threadIdx.x < npop) score[threadIdx.x] = 0;
-    __syncthreads();
-    for (int pos = threadIdx.x; pos < n; pos += blockDim.x) {
-        const int e = order[pos];  // its walks' slots at wslots[e * gtail + g] (gtail = the record layout's groups)
-        uint32_t sc;
-        if (pos < whole) {
-            sc = 5u * wslots[e * gtail];
-        } else {
-            uint32_t sum = 0;
-            for (int g = 0; g < gtail; ++g) sum += wslots[e * gtail + g];
-            sc = 4u * sum;
-        }
-        atomicMax(&score[e / pop_eps], sc);
-    }
-    __syncthreads();  // every read of the old order precedes the writes below
-    if (threadIdx.x == 0) {  // populations by (score, index), lightest first
-        for (int k = 0; k < npop; ++k) rank[k] = k;
-        for (int i = 1; i < npop; ++i)
-            for (int j = i; j > 0 && score[rank[j]] < score[rank[j - 1]]; --j) {
-                const int t = rank[j];
-                rank[j] = rank[j - 1];
-                rank[j - 1] = t;
-            }
-    }
-    __syncthreads();
-    for (int pos = threadIdx.x; pos < n; pos += blockDim.x) order[pos] = rank[pos / pop_eps] * pop_eps + pos % pop_eps;
-}
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
 // per walk, whole populations of equal-length episodes, a caller's order array
 static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, const GenomeSrc& src) {
@@ -2334,10 +2382,13 @@ static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, con
 }
 
 // table + path scan (+ the generation tail when step.st) for one batch
+// rj_out: a training launch with the walk-order feedback hands its job here
+// instead of launching it; rj_in: a job to run inside (or after) this launch
 static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                         const sgmm_env_params* params, const GenomeSrc& src, bool arl,
                         int32_t hidden, double* fitness, int32_t* trades, void* workspace,
-                        size_t workspace_bytes, const StepArgs& step, hipStream_t s) {
+                        size_t workspace_bytes, const StepArgs& step, hipStream_t s,
+                        ReorderJob* rj_out = nullptr, const ReorderJob* rj_in = nullptr) {
     SGMM_REQUIRE(fitness && trades, "null fitness/trades output");
     if (eps->n == 0) return SGMM_OK;
     const int32_t nsi = eps->inv_max - eps->inv_min + 1;
@@ -2366,6 +2417,8 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n));
     }
     EpArrays ep = ep_arrays(eps, arl);
+    const ReorderJob* rj_fold = nullptr;
+    bool rj_done = false;
     const bool fr = use_frontier(arl, hidden, eps);
     const FrontierPlan plan = frontier_plan(eps->n);
     if (fr) {
@@ -2389,15 +2442,19 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);
         const bool valu = table_valu();
+        // the job may ride along only if this launch's workspace use ends below its slot counts
+        if (rj_in && rj_in->order &&
+            reinterpret_cast<const char*>(rj_in->wslots) >= w + rollout_ws_bytes(eps->n, eps->total_steps, nsi, arl))
+            rj_fold = rj_in;
         switch (hidden) {
             case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew); break;
             case 16:
                 if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
-                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
+                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
                 break;
             case 32:
                 if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
-                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
+                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
                 break;
             default:
                 if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
@@ -2446,8 +2503,16 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     SGMM_LAUNCHED();
     if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src)) {
-        SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, wslots, const_cast<int32_t*>(eps->order), eps->n,
-                    plan.whole, plan.gtail, src.pop_eps);
+        const ReorderJob job{wslots, const_cast<int32_t*>(eps->order), eps->n, plan.whole, plan.gtail, src.pop_eps};
+        if (rj_out) {
+            *rj_out = job;
+        } else {
+            SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, job);
+            SGMM_LAUNCHED();
+        }
+    }
+    if (rj_in && rj_in->order && !rj_done) {  // the job did not ride along: on its own
+        SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, *rj_in);
         SGMM_LAUNCHED();
     }
     return SGMM_OK;
@@ -2547,7 +2612,8 @@ extern "C" int sgmm_generation_multi(const sgmm_ticks* ticks, const sgmm_episode
 // pre-tell master and the scan's workgroup k writes the new master (mode 4)
 static int validate_impl(const sgmm_ticks* ticks, const sgmm_episodes* val_eps, const sgmm_env_params* params,
                          const sgmm_populations* pops, double* val_fitness, int32_t* val_trades, void* workspace,
-                         size_t workspace_bytes, hipStream_t s, bool deferred = false) {
+                         size_t workspace_bytes, hipStream_t s, bool deferred = false,
+                         const ReorderJob* rj = nullptr) {
     const int32_t H = pops->hidden, K = pops->n_pop;
     if (int rc = check_episodes(ticks, val_eps, params, pops->masters_mm, H)) return rc;
     SGMM_REQUIRE(val_eps->n == K, "validation episodes must be one per population (%d), got %d", K, val_eps->n);
@@ -2565,7 +2631,7 @@ static int validate_impl(const sgmm_ticks* ticks, const sgmm_episodes* val_eps, 
                   n_mm, (deferred && arl) ? (int64_t)kAdvGenome : 0, 0, pops->history, pops->history_cap, 1, 1,
                   pops->seeds, deferred ? 4 : 2};
     return rollout_impl(ticks, val_eps, params, src, false, H, val_fitness, val_trades, workspace, workspace_bytes,
-                        step, s);
+                        step, s, nullptr, rj);
 }
 
 extern "C" int sgmm_validate_multi(const sgmm_ticks* ticks, const sgmm_episodes* val_eps,
@@ -2603,10 +2669,12 @@ extern "C" int sgmm_generation_multi_best(const sgmm_ticks* ticks, const sgmm_ep
     StepArgs step{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, n_mm, n_adv, 0,
                   pops->history, pops->history_cap, P, P, pops->seeds, 3};
     hipStream_t s = as_stream(stream);
+    ReorderJob job{nullptr, nullptr, 0, 0, 0, 1};
     if (int rc = rollout_impl(ticks, train_eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
-                              step, s))
+                              step, s, &job))
         return rc;
-    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s, true);
+    return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s, true,
+                         &job);
 }
 
 extern "C" int sgmm_rollout_fitness_asked_multi(const sgmm_ticks* ticks, const sgmm_episodes* eps,
