@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "sgmm_rollout.h"
@@ -724,6 +725,7 @@ struct ReorderJob {
     const uint32_t* wslots;
     int32_t* order;  // null: no job
     int32_t n, whole, gtail, pop_eps;
+    uint32_t w_whole = 5, w_split = 4;  // score weights (SGMM_REORDER_WEIGHTS=whole,split for experiments)
 };
 __device__ __forceinline__ void walk_reorder_block(const ReorderJob rj) {
     const uint32_t* __restrict__ wslots = rj.wslots;
@@ -752,11 +754,11 @@ __device__ __forceinline__ void walk_reorder_block(const ReorderJob rj) {
             sc[j] = 0;
             if (e[j] < 0) continue;
             if (pos < whole) {
-                sc[j] = 5u * wslots[e[j] * gtail];
+                sc[j] = rj.w_whole * wslots[e[j] * gtail];
             } else {
                 uint32_t sum = 0;
                 for (int g = 0; g < gtail; ++g) sum += wslots[e[j] * gtail + g];
-                sc[j] = 4u * sum;
+                sc[j] = rj.w_split * sum;
             }
         }
         // one LDS atomic per wave where its 64 positions are one population (the usual
@@ -2503,7 +2505,14 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     }
     SGMM_LAUNCHED();
     if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src)) {
-        const ReorderJob job{wslots, const_cast<int32_t*>(eps->order), eps->n, plan.whole, plan.gtail, src.pop_eps};
+        ReorderJob job{wslots, const_cast<int32_t*>(eps->order), eps->n, plan.whole, plan.gtail, src.pop_eps};
+        if (const char* v = std::getenv("SGMM_REORDER_WEIGHTS")) {
+            unsigned a = 0, b = 0;
+            if (std::sscanf(v, "%u,%u", &a, &b) == 2 && a > 0 && b > 0 && a < 64 && b < 64) {
+                job.w_whole = a;
+                job.w_split = b;
+            }
+        }
         if (rj_out) {
             *rj_out = job;
         } else {
