@@ -2119,7 +2119,9 @@ static FrontierPlan frontier_plan(int32_t n) {
         return !(v && std::strcmp(v, "0") == 0);
     }();
     const int64_t r = n % S;
-    if (tail && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
+    const char* fw = std::getenv("SGMM_FRONTIER_FOUR");  // experiments: 0 = no four-walk rule
+    const bool four = !(fw && std::strcmp(fw, "0") == 0);
+    if (tail && four && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
         // from 2.5 episodes per SIMD up to 4: four walks per SIMD, 2n - 4S whole
         // and the rest in halves, one whole and three half walks per SIMD (config
         // 3: 2560 = 1024 whole + 1536 in halves; 660.5-668.0 against 670.3-670.6 us
