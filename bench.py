@@ -97,7 +97,20 @@ def parse():
                          "(ceil(P/N) individuals per population; no exchange) and label the line '1 of N ranks'")
     ap.add_argument("--val-mode", default="auto", choices=("auto", "fused", "best"),
                     help="DRLEngine val_mode (auto: best from 256 individuals per population shard)")
+    ap.add_argument("--plan", default="",
+                    help="launch-plan overrides for A/B runs, e.g. 'groups=2,spill=0' (sgmm_plan_set; "
+                         "knobs: " + "policy_path groups lane_split tail four min_eps table_sp scan_threads "
+                         "reorder_weights spill" + "); recorded in the line's config")
+    ap.add_argument("--no-walk-feedback", action="store_true", help="DRLEngine(walk_feedback=False)")
     return ap.parse_args()
+
+
+def parse_plan(text):
+    out = {}
+    for kv in filter(None, (x.strip() for x in text.split(","))):
+        k, v = kv.split("=", 1)
+        out[k.strip()] = v.strip() if k.strip() == "policy_path" else int(v)
+    return out
 
 
 def workload_spec(args):
@@ -218,6 +231,23 @@ def latest_pmc(path_arg, config):
         return None
 
 
+def latest_trace_window(config, kname):
+    """The committed rocprofv3 kernel-trace measurement of the policy kernel over
+    the same command's timed window (profiles/rNN_kernel_window_cC.txt, written by
+    tools/kt_window.py from `rocprofv3 --kernel-trace` of `bench.py --config C`)."""
+    import re
+    cands = sorted((ROOT / "profiles").glob(f"r*_kernel_window_c{config}.txt"))
+    if not cands:
+        return None
+    fam = "k_policy_frontier" if kname == "policy_frontier" else "k_policy_table"
+    for line in cands[-1].read_text().splitlines():
+        m = re.search(r"window mean\s+([0-9.]+) us over (\d+) dispatches", line)
+        if m and fam in line:
+            return {"us": float(m.group(1)), "dispatches": int(m.group(2)), "kernel": line.split("(")[0].strip(),
+                    "source": str(cands[-1].relative_to(ROOT))}
+    return None
+
+
 def _series(per_gen, kname, g0):
     """One kernel's per-generation time over the profiled window: first, last,
     mean, min, max (us) and the generations they cover."""
@@ -228,12 +258,13 @@ def _series(per_gen, kname, g0):
             "min": min(us), "max": max(us)}
 
 
-def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, val_mode, seed0=1234):
+def make_engine(sgmm, spec, P_glob, save_dir, dist, use_graph, val_mode, seed0=1234, walk_feedback=True):
     import torch
     torch.manual_seed(seed0)
     engines = [sgmm.DRLEngine(pop_size=P_glob, phi=phi, tick_size=tick, fee_rate=0.0, use_arl=spec["arl"],
                               save_dir=save_dir, hidden_dim=spec["H"], rng="device", seed=seed0 + 17 * k,
-                              val_mode=val_mode, sync_every=10**9, verbose=False, use_graph=use_graph, dist=dist)
+                              val_mode=val_mode, sync_every=10**9, verbose=False, use_graph=use_graph, dist=dist,
+                              walk_feedback=walk_feedback)
                for k, (phi, tick, _) in enumerate(spec["pops"])]
     return sgmm.MultiDRLEngine(engines)
 
@@ -261,6 +292,9 @@ def main():
     sgmm = sgmm_pkg.load()
     from sgmm_amd import _lib
     from sgmm_amd.shard import shard_capacity
+    plan = parse_plan(args.plan)
+    if plan:
+        _lib.plan_set(**plan)
 
     P, H, T, Tv = spec["P"], spec["H"], spec["T"], spec["Tv"]
     shard_of = max(1, args.shard_of)
@@ -280,7 +314,8 @@ def main():
             dist.barrier()
 
     tmp = tempfile.mkdtemp(prefix="sgmm_bench_")
-    eng = make_engine(sgmm, spec, P_glob, tmp, None, not args.no_graph, args.val_mode)
+    eng = make_engine(sgmm, spec, P_glob, tmp, None, not args.no_graph, args.val_mode,
+                      walk_feedback=not args.no_walk_feedback)
     sess = eng.session(tr, va, st, generations=args.warmup + args.steps)
     sess.steps(0, args.warmup)
     sess.capture()  # graphs recorded (not run) before the timed region
@@ -311,7 +346,8 @@ def main():
     n_rank = shard_capacity(P_glob, world)
     g0 = args.warmup
     n_prof = args.steps if args.profile_steps <= 0 else min(args.steps, max(args.profile_steps, 1))
-    peng = make_engine(sgmm, spec, n_rank, tmp, False, False, args.val_mode)  # the timed run's seeds
+    peng = make_engine(sgmm, spec, n_rank, tmp, False, False, args.val_mode,  # the timed run's seeds
+                       walk_feedback=not args.no_walk_feedback)
     psess = peng.session(tr, va, st, generations=g0 + n_prof)
     for g in range(g0):
         psess.step(g)
@@ -366,6 +402,13 @@ def main():
                                     "note": note},
                     "avg_launch_us": tab["avg_us"],
                     "launch_us_over_timed_window": _series(per_gen, kname, g0)}
+        tw = latest_trace_window(args.config, kname) if shard_of == 1 else None
+        if tw:
+            # the same frac from the committed rocprof trace of this command (timed window)
+            tw["frac"] = steps_per_launch * fl / (tw["us"] * 1e-6) / 1e12 / FP32_PEAK_TFLOPS
+            tw["note"] = ("rocprofv3 --kernel-trace of `bench.py --config %d` on a previous box, dispatches of "
+                          "the timed window only (tools/kt_window.py); the live frac above is this run's" % args.config)
+            roofline["trace_window"] = tw
         if traffic:
             gbps = traffic / (tab["avg_us"] * 1e-6) / 1e9
             roofline["hbm"] = {"achieved_GBps": gbps, "peak_GBps": HBM_PEAK_GBPS,
@@ -374,6 +417,15 @@ def main():
 
     if rank == 0:
         gens_per_s = args.steps / dt
+        if cpu:
+            # the other half of BASELINE's metric: generations per second of the same
+            # workload on the CPU path = its env-steps/s / the workload's training
+            # env-steps per generation (every population, the reference's Pool loop)
+            steps_per_gen = K * P_glob * T
+            cpu["generations_per_s"] = cpu["value"] / steps_per_gen
+            cpu["env_steps_per_generation"] = steps_per_gen
+            cpu["gpu_generations_per_s"] = gens_per_s
+            cpu["generations_speedup"] = gens_per_s / cpu["generations_per_s"]
         out = {
             # a shard line is ONE rank's share of a strong-scaled run: its own metric
             # name and config id, so it cannot be taken for the whole config
@@ -393,7 +445,9 @@ def main():
                        "parallelism": f"population shards x{world}" + (" + RCCL all-gather" if world > 1 else ""),
                        "hip_graph": bool(sess.use_graph),
                        "graph_has_exchange": bool(sess.full_graph) if world > 1 else None,
-                       "graph_capture_error": getattr(sess, "capture_error", None)},
+                       "graph_capture_error": getattr(sess, "capture_error", None),
+                       "plan_overrides": plan or None,
+                       "walk_feedback": not args.no_walk_feedback},
             "generations_per_s": gens_per_s,
             "roofline": roofline,
             "cpu_baseline": cpu,

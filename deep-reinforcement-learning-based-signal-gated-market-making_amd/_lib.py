@@ -17,7 +17,7 @@ import torch  # noqa: F401  (must precede loading libsgmm.so, see module doc)
 
 PKG_DIR = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("SGMM_LIB", PKG_DIR / "libsgmm.so"))
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class SgmmError(RuntimeError):
@@ -66,7 +66,7 @@ class Populations(ctypes.Structure):
     _fields_ = [("n_pop", ctypes.c_int32), ("P", ctypes.c_int32), ("hidden", ctypes.c_int32),
                 ("history_cap", ctypes.c_int32)] + \
         [(n, ctypes.c_void_p) for n in ("states", "masters_mm", "masters_adv", "best_masters", "seeds",
-                                        "history")]
+                                        "history", "walk_order")]
 
 
 class DayStreams(ctypes.Structure):
@@ -91,7 +91,7 @@ class GAHistory(ctypes.Structure):
 assert ctypes.sizeof(EnvParams) == 48
 assert ctypes.sizeof(GAState) == 80
 assert ctypes.sizeof(GAHistory) == 40
-assert ctypes.sizeof(Populations) == 64
+assert ctypes.sizeof(Populations) == 72
 
 _VP, _I32, _I64, _U32, _U64, _D, _SZ = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64,
                                         ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double,
@@ -143,6 +143,8 @@ SIGNATURES = {
     "sgmm_sgu2_forward": (ctypes.c_int, [_VP, _I32, _VP, _I64, _I32, _VP, _VP, _VP, _VP]),
     "sgmm_step_bundle": (ctypes.c_int, [ctypes.POINTER(EventBars), _I32, _VP, _VP, _VP, _I32, _VP, _VP, _VP,
                                         _VP, _VP, _VP]),
+    "sgmm_plan_set": (ctypes.c_int, [_I32, _I32]),
+    "sgmm_plan_get": (ctypes.c_int, [_I32]),
     "sgmm_profile_enable": (ctypes.c_int, [ctypes.c_int]),
     "sgmm_profile_read": (ctypes.c_int, [ctypes.c_int, _VP, _VP, _VP]),
 }
@@ -211,3 +213,42 @@ def profile_read(max_kinds: int = 32) -> dict:
     raw = names.raw
     return {raw[48 * i:48 * i + 48].split(b"\0", 1)[0].decode(): (float(tot[i]), int(cnt[i]))
             for i in range(n)}
+
+
+# launch-plan overrides (include/sgmm.h SGMM_PLAN_*): tests and A/B experiments
+PLAN_KNOBS = {"policy_path": 0, "groups": 1, "lane_split": 2, "tail": 3, "four": 4, "min_eps": 5,
+              "table_sp": 6, "scan_threads": 7, "reorder_weights": 8, "spill": 9}
+POLICY_PATHS = {"auto": -1, "frontier": 1, "table": 2, "valu": 3}
+
+
+def plan_set(**knobs) -> dict:
+    """Set launch-plan overrides (None or a negative value = the default rule);
+    returns the previous values.  policy_path takes "auto" / "frontier" /
+    "table" / "valu".  Applies to launches enqueued (or graphs captured) after
+    the call."""
+    L = load()
+    prev = {}
+    for k, v in knobs.items():
+        if k not in PLAN_KNOBS:
+            raise SgmmError(f"unknown plan knob {k!r}")
+        if k == "policy_path" and isinstance(v, str):
+            v = POLICY_PATHS[v]
+        prev[k] = L.sgmm_plan_get(PLAN_KNOBS[k])
+        check(L.sgmm_plan_set(PLAN_KNOBS[k], -1 if v is None else int(v)), "sgmm_plan_set")
+    return prev
+
+
+class plan:
+    """Context manager: `with plan(groups=2, policy_path="frontier"): ...`"""
+
+    def __init__(self, **knobs):
+        self.knobs = knobs
+        self.prev = None
+
+    def __enter__(self):
+        self.prev = plan_set(**self.knobs)
+        return self
+
+    def __exit__(self, *exc):
+        plan_set(**self.prev)
+        return False

@@ -28,12 +28,16 @@ def build_library(force: bool = False, verbose: bool = False, extra_flags: list[
                   out: Path | None = None) -> Path:
     out = Path(out) if out else PKG_DIR / "libsgmm.so"
     deps = [PKG_DIR / s for s in SOURCES + HEADERS]
-    if not force and out.exists() and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps):
-        return out
     flags = FLAGS + list(extra_flags or [])
+    tag = hashlib.sha1(" ".join([HIPCC, *flags]).encode()).hexdigest()[:10]
+    # the flag set a library was linked with sits beside it (libsgmm.so.flags):
+    # a library is up to date only for the same flags and newer than every source
+    side = out.with_name(out.name + ".flags")
+    if (not force and out.exists() and side.exists() and side.read_text().strip() == tag
+            and all(out.stat().st_mtime >= d.stat().st_mtime for d in deps)):
+        return out
     # objects are cached per flag set (build/ is git-ignored): a translation
     # unit is recompiled when it or any shared header is newer than its object
-    tag = hashlib.sha1(" ".join([HIPCC, *flags]).encode()).hexdigest()[:10]
     obj_dir = PKG_DIR / "build" / tag
     obj_dir.mkdir(parents=True, exist_ok=True)
     objs = [obj_dir / (Path(s).stem + ".o") for s in SOURCES]
@@ -57,6 +61,7 @@ def build_library(force: bool = False, verbose: bool = False, extra_flags: list[
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(str(out) + ".tmp", out)
+    side.write_text(tag + "\n")
     return out
 
 

@@ -1,4 +1,7 @@
 // sgmm_capi.hip -- ABI version, thread-local error reporting, kernel timing.
+#include <atomic>
+#include <climits>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -32,7 +35,42 @@ hipEvent_t take_event() {
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
 }
+// launch-plan overrides (sgmm_plan_set), -1 = the default rule
+std::atomic<int32_t> g_plan[SGMM_PLAN_N];
+std::once_flag g_plan_once;
+void plan_init() {
+    for (auto& v : g_plan) v.store(-1, std::memory_order_relaxed);
+#ifdef SGMM_EXPERIMENTS
+    // the A/B variant build: initial values from the environment (tools/)
+    auto env = [](const char* n) -> int32_t {
+        const char* v = std::getenv(n);
+        return v && *v ? (int32_t)std::atoi(v) : -1;
+    };
+    if (const char* v = std::getenv("SGMM_TABLE_PATH")) {
+        const int32_t p = !std::strcmp(v, "frontier") ? 1 : !std::strcmp(v, "table") ? 2 : !std::strcmp(v, "valu") ? 3 : -1;
+        g_plan[SGMM_PLAN_POLICY_PATH].store(p);
+    }
+    g_plan[SGMM_PLAN_GROUPS].store(env("SGMM_FRONTIER_NW"));
+    g_plan[SGMM_PLAN_LANE_SPLIT].store(env("SGMM_FRONTIER_LS"));
+    g_plan[SGMM_PLAN_TAIL].store(env("SGMM_FRONTIER_TAIL"));
+    g_plan[SGMM_PLAN_FOUR].store(env("SGMM_FRONTIER_FOUR"));
+    g_plan[SGMM_PLAN_MIN_EPS].store(env("SGMM_FRONTIER_MIN_EPS"));
+    g_plan[SGMM_PLAN_TABLE_SP].store(env("SGMM_TABLE_SP"));
+    g_plan[SGMM_PLAN_SCAN_THREADS].store(env("SGMM_SCAN_THREADS"));
+    g_plan[SGMM_PLAN_SPILL].store(env("SGMM_FRONTIER_SPILL"));
+    if (const char* v = std::getenv("SGMM_REORDER_WEIGHTS")) {
+        unsigned a = 0, b = 0;
+        if (std::sscanf(v, "%u,%u", &a, &b) == 2 && a > 0 && b > 0 && a < 64 && b < 64)
+            g_plan[SGMM_PLAN_REORDER_WEIGHTS].store((int32_t)(a << 8 | b));
+    }
+#endif
+}
 }  // namespace
+
+int32_t plan_value(int k) {
+    std::call_once(g_plan_once, plan_init);
+    return (k >= 0 && k < SGMM_PLAN_N) ? g_plan[k].load(std::memory_order_relaxed) : -1;
+}
 
 void set_error(const char* fmt, ...) {
     va_list ap;
@@ -81,6 +119,23 @@ using namespace sgmm;
 extern "C" int sgmm_abi_version(void) { return SGMM_ABI_VERSION; }
 
 extern "C" const char* sgmm_last_error(void) { return sgmm::g_err; }
+
+extern "C" int sgmm_plan_set(int32_t knob, int32_t value) {
+    clear_error();
+    SGMM_REQUIRE(knob >= 0 && knob < SGMM_PLAN_N, "unknown plan knob %d", knob);
+    (void)plan_value(knob);  // initialised
+    g_plan[knob].store(value < 0 ? -1 : value, std::memory_order_relaxed);
+    return SGMM_OK;
+}
+
+extern "C" int sgmm_plan_get(int32_t knob) {
+    clear_error();
+    if (knob < 0 || knob >= SGMM_PLAN_N) {
+        set_error("unknown plan knob %d", knob);
+        return INT32_MIN;
+    }
+    return plan_value(knob);
+}
 
 extern "C" int sgmm_profile_enable(int enable) {
     std::lock_guard<std::mutex> lk(g_prof_mu);

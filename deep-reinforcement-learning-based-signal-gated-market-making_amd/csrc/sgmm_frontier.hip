@@ -88,6 +88,13 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     // successor (bits 9-11) and the fill (bit 12) written back by the column
     __shared__ uint16_t pl[kWave * (NSI - 1)];
     __shared__ uint32_t nslot_s;  // MLP slots run (FrontierArgs::wslots; in LDS: the walk loop has no register to spare)
+    // spill bookkeeping in LDS (no register is spare in the walk loop): this wave's
+    // id, the first tick offset it may stop at, its slot budget
+    __shared__ uint32_t wid_s, tmin_s, sbud_s;
+    if (threadIdx.x == 0) {  // every wave of the launch writes its spill entry, spilled or not
+        wid_s = blockIdx.x;
+        if (args.wspill) args.wspill[blockIdx.x] = 0u;
+    }
 
     const sgmm_ticks& tk = args.tk;
     const EpArrays& ep = args.ep;
@@ -105,10 +112,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     const int off = ((int)blockIdx.x % LS) * NL;  // this wave's first chunk within the group
     const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
-    if (T <= 0) return;  // block-uniform
-    const int CL = frontier_len(T, nw);
+    const int CL = frontier_len(max(T, 1), nw);
     const int nch = (T + CL - 1) / CL;
-    if (cg * kFrontierLanes + off >= nch) return;  // a group (part) past the episode's last chunk
+    if (T <= 0 || cg * kFrontierLanes + off >= nch) {  // block-uniform: no chunk here
+        // (a walk with no chunk still has a slot count for the walk-order feedback: 0)
+        if (LS == 1 && threadIdx.x == 0 && args.wslots)
+            args.wslots[frontier_rec(e, ep.ngrp, cg * kFrontierLanes + off) / NL] = 0u;
+        return;
+    }
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const bool lane_ok = LS == 1 || lane < NL;
     const int c = cg * kFrontierLanes + off + lane;    // this lane's chunk
@@ -184,7 +195,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
     int fr_extra = 0;
-    if (LS == 1 && lane == 0) nslot_s = 0;
+    if (lane == 0) {
+        nslot_s = 0;
+        sbud_s = args.spill_budget;
+        tmin_s = args.spill_budget ? (uint32_t)max(4, CL - kSpillTicks) : 0xFFFFFFFFu;
+    }
 
     // layers 1-3 for the columns of this slot (their inputs in the rows of
     // hb as (s1, s2, inv/2, 0)); tiles >= NQ are skipped; o0 / o1 = the
@@ -274,6 +289,21 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_b);
 #endif
+        // spill: a walk past the launch's slot budget stops here once its chunks
+        // have at most kSpillTicks ticks left; k_frontier_spill finishes them
+        // tick-parallel from the records written below (every 4 ticks)
+        if ((tt & 3) == 0 && (uint32_t)tt >= (uint32_t)__builtin_amdgcn_readfirstlane((int)tmin_s)) {
+            const uint32_t ns = (uint32_t)__builtin_amdgcn_readfirstlane(
+                (int)__hip_atomic_load(&nslot_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+            if (ns > (uint32_t)__builtin_amdgcn_readfirstlane((int)sbud_s)) {
+                if (lane == 0) {
+                    args.wspill[wid_s] = (uint32_t)tt;
+                    // the walk-order feedback's count: extrapolated to the whole walk
+                    nslot_s = (uint32_t)((uint64_t)ns * (uint32_t)CL / (uint32_t)tt);
+                }
+                break;
+            }
+        }
         const bool act = tt < ntl;
         const float s1 = ns1, s2 = ns2;
         const int64_t tcur = ti;
@@ -316,7 +346,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         // apart: a heavy walk, the launch's tail) takes the SIMD's issue
         // priority over the light walks beside it (round 4, profiles/r04_ab)
         fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
-        if (LS == 1 && lane == 0)  // (the walk-order feedback is for one wave per walk)
+        if (lane == 0)
             __hip_atomic_fetch_add(&nslot_s, (uint32_t)((any0 ? 1 : 0) + nx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         if ((tt & 7) == 7) {
             if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
@@ -520,6 +550,266 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         if (LS == 1 && lane == 0 && args.wslots)
             args.wslots[ci / NL] = __hip_atomic_load(&nslot_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     }
+}
+
+// ------------------------------------------------------------------ spill: the rest of the heavy walks
+// The frontier launch ends with its heaviest walks: policies whose paths rarely
+// merge run up to five MLP slots per tick, serially, while the SIMDs around them
+// have run dry (config 3: the last SIMD ends ~570 us into the launch, the median
+// one at ~400 us, profiles/r05_timeline/tlo_g15_default.txt).  A walk that passes
+// the launch's slot budget therefore stops at a tick offset K (a multiple of 4,
+// once its chunks have at most kSpillTicks ticks left), leaving its records as
+// they stand -- per chunk the map of the tracked start states to their states at
+// K, the trade counts so far, the merge tick -- and K in wspill[its wave id].
+// This kernel, stream-ordered after the walk launch, runs the remaining ticks of
+// every spilled chunk tick-parallel: all inventory states of each tick, one wave
+// per state (the state-parallel table's arithmetic, k_policy_table_sp), lanes =
+// (chunk, tick) in segments of 16 / 32 / 64 ticks, then a segmented map scan
+// composes each chunk's path from its state at K, and the kernel writes the plane
+// rows of ticks K.. (every tracked start's plane, or p0's after the merge), the
+// final map and the completed trade counts in the frontier layout -- exactly what
+// the walk would have written, so the path scan reads them unchanged.
+// Fixed grid (graph-capturable): every workgroup reads the launch's entries, ranks
+// the spilled waves identically, and takes a contiguous range of the work items
+// (spilled wave, 4 of its chunks); with nothing spilled it exits after one load.
+constexpr int kSpillBlocks = 512;  // two workgroups per CU (54-83 KB of LDS each)
+// wave_map_scan_seg for a runtime segment width (wave-uniform: every lane takes the same steps)
+__device__ __forceinline__ uint64_t m_scan_seg(uint64_t m, int seg) {
+    if (seg >= 64) return wave_map_scan_seg<64>(m);
+    if (seg >= 32) return wave_map_scan_seg<32>(m);
+    return wave_map_scan_seg<16>(m);
+}
+template <int H, int NSI>
+__global__ __launch_bounds__(kWave * NSI) void k_frontier_spill(FrontierArgs args, int32_t n_waves, int32_t ls) {
+    static_assert(H % 16 == 0 && H <= 32, "spill: H = 16 or 32");
+    using L = GenomeLayout<H>;
+    constexpr int NT = H / 16, KS = H / 4, HP = H + 4;
+    constexpr int kPer = 16;   // entries per thread and segment
+    constexpr int kCap = 512;  // spilled waves per window
+    const EpArrays& ep = args.ep;
+    const int tid = (int)threadIdx.x, nt = (int)blockDim.x, wv = tid >> 6, lane = tid & (kWave - 1);
+    const int grp = lane >> 4, col = lane & 15;
+    const int nwv = nt >> 6;
+    const int NL = kFrontierLanes / ls;
+    const int ipw = NL / 4;  // work items per spilled wave: 4 chunks each
+    const int32_t inv_min = args.inv_min, nsi = args.nsi;
+    __shared__ uint32_t list_s[kCap];
+    __shared__ uint32_t wcnt_s[kPer][NSI];
+    __shared__ __attribute__((aligned(16))) float gsm[L::N];
+    __shared__ __attribute__((aligned(16))) float w3i[2 * H];
+    __shared__ __attribute__((aligned(16))) float hb_s[NSI][kWave * HP];
+    __shared__ __attribute__((aligned(16))) double rl_s[NSI][kWave];
+    __shared__ uint8_t to_s[NSI][kWave];  // successor state | traded << 7
+    int staged = -1;                      // the episode whose genome is in gsm
+    float w2f[NT][KS];
+    f32x4 b2c[NT];
+    for (int seg0 = 0; seg0 < n_waves; seg0 += kPer * nt) {
+        // this segment's entries in registers, ranked by (k, thread): the same
+        // order in every workgroup
+        uint32_t ent[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int b = seg0 + k * nt + tid;
+            ent[k] = b < n_waves ? args.wspill[b] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const uint64_t m = __ballot(ent[k] != 0u);
+            if (lane == 0) wcnt_s[k][wv] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        uint32_t total = 0, rank[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            uint32_t before = 0;
+            for (int w = 0; w < nwv; ++w) {
+                if (w == wv) before = total;
+                total += wcnt_s[k][w];
+            }
+            rank[k] = before + (uint32_t)mbcnt64(__ballot(ent[k] != 0u));
+        }
+        __syncthreads();  // wcnt_s is rewritten by the next segment
+        for (uint32_t r0 = 0; r0 < total; r0 += kCap) {
+#pragma unroll
+            for (int k = 0; k < kPer; ++k)
+                if (ent[k] && rank[k] >= r0 && rank[k] < r0 + kCap) list_s[rank[k] - r0] = (uint32_t)(seg0 + k * nt + tid);
+            __syncthreads();
+            const int m = (int)min(total - r0, (uint32_t)kCap);
+            const int items = m * ipw;
+            const int per = (items + (int)gridDim.x - 1) / (int)gridDim.x;
+            const int i0 = (int)blockIdx.x * per, i1 = min(items, i0 + per);
+            for (int it = i0; it < i1; ++it) {
+                const int b = (int)list_s[it / ipw], q = it % ipw;
+                int pos, cg, nw;
+                frontier_wave(ep, b / ls, pos, cg, nw);
+                const int off = (b % ls) * NL;
+                const int e = __builtin_amdgcn_readfirstlane(ep.order ? ep.order[pos] : pos);
+                const int32_t T = ep.len[e];
+                const int CL = frontier_len(T, nw);
+                const int nch = (T + CL - 1) / CL;
+                const int K = __builtin_amdgcn_readfirstlane((int)args.wspill[b]);
+                const int R = CL - K;  // remaining ticks of a full chunk (1..kSpillTicks)
+                const int SEG = __builtin_amdgcn_readfirstlane(R <= 16 ? 16 : (R <= 32 ? 32 : 64));
+                const int shs = SEG == 16 ? 4 : (SEG == 32 ? 5 : 6);
+                const int cpp = kWave / SEG;  // chunks per pass
+                const int64_t tb = ep.tick_off[e], so = ep.step_off[e];
+                const int64_t rbase = frontier_base(so, e, ep.ngrp) + (int64_t)cg * CL * kFrontierLanes;
+                if (e != staged) {  // block-uniform
+                    __syncthreads();
+                    stage_genomes(args.src, e, ep.genome[e], -1, L::N, gsm, nullptr);
+                    __syncthreads();
+                    if (tid < 2 * H) w3i[tid] = gsm[L::W3 + (tid & 1) * H + (tid >> 1)];
+#pragma unroll
+                    for (int rt = 0; rt < NT; ++rt) {
+#pragma unroll
+                        for (int i = 0; i < KS; ++i) w2f[rt][i] = gsm[L::W2 + (16 * rt + col) * H + 4 * i + grp];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) b2c[rt][r] = gsm[L::B2 + 16 * rt + 4 * grp + r];
+                    }
+                    staged = e;
+                    __syncthreads();
+                }
+                const sgmm_env_params p = args.params[ep.param[e]];
+                for (int pass = 0; pass < 4 / cpp; ++pass) {
+                    // sample s = lane: chunk (within the wave's NL) q*4 + pass*cpp + s/SEG, tick offset K + s%SEG
+                    auto tick_of = [&](int smp, bool& ok, int& lg) {
+                        const int ch = 4 * q + pass * cpp + (smp >> shs);
+                        lg = off + ch;
+                        const int c = cg * kFrontierLanes + lg, tt = K + (smp & (SEG - 1));
+                        ok = c < nch && c * CL + tt < T && tt < CL;
+                        return tb + min((int64_t)c * CL + tt, (int64_t)T - 1);
+                    };
+                    const int si = wv;
+                    float xs0[4], xs1[4];
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq) {
+                        bool ok;
+                        int lg;
+                        const int64_t ti = tick_of(16 * qq + col, ok, lg);
+                        xs0[qq] = args.tk.s1n[ti];
+                        xs1[qq] = args.tk.s2n[ti];
+                    }
+                    bool valid;
+                    int lg;
+                    const int64_t tix = tick_of(lane, valid, lg);
+                    const double tmid = args.tk.mid_next[tix], task = args.tk.best_ask[tix], tbid = args.tk.best_bid[tix];
+                    const double tbmax = args.tk.buy_max[tix], tsmin = args.tk.sell_min[tix];
+                    const float x2 = (float)((double)(inv_min + si) / 2.0);
+                    float h1[KS][4];
+#pragma unroll
+                    for (int i = 0; i < KS; ++i) {
+                        const int k = 4 * i + grp;
+                        const float a0 = gsm[L::W1 + 3 * k], a1 = gsm[L::W1 + 3 * k + 1], bb = gsm[L::B1 + k];
+                        const float w1s = gsm[L::W1 + 3 * k + 2];
+#pragma unroll
+                        for (int qq = 0; qq < 4; ++qq)
+                            h1[i][qq] = relu(__builtin_fmaf(w1s, x2, __builtin_fmaf(a1, xs1[qq], __builtin_fmaf(a0, xs0[qq], bb))));
+                    }
+                    f32x4 acc[4][NT];
+#pragma unroll
+                    for (int i = 0; i < KS; ++i)
+#pragma unroll
+                        for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+                            for (int rt = 0; rt < NT; ++rt)
+                                acc[qq][rt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w2f[rt][i], h1[i][qq],
+                                                                                   i == 0 ? b2c[rt] : acc[qq][rt], 0, 0, 0);
+                    float* hb = hb_s[si];
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+                        for (int rt = 0; rt < NT; ++rt) {
+                            f32x4 v;
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) v[r] = relu(acc[qq][rt][r]);
+                            *reinterpret_cast<f32x4*>(&hb[(16 * qq + col) * HP + 16 * rt + 4 * grp]) = v;
+                        }
+                    float o0 = gsm[L::B3], o1 = gsm[L::B3 + 1];
+#pragma unroll
+                    for (int j4 = 0; j4 < H / 4; ++j4) {
+                        const f32x4 h = *reinterpret_cast<const f32x4*>(&hb[lane * HP + 4 * j4]);
+#pragma unroll
+                        for (int r2 = 0; r2 < 2; ++r2) {
+                            const f32x4 w = *reinterpret_cast<const f32x4*>(&w3i[2 * (4 * j4 + 2 * r2)]);
+                            o0 = __builtin_fmaf(w[0], h[2 * r2], o0);
+                            o1 = __builtin_fmaf(w[1], h[2 * r2], o1);
+                            o0 = __builtin_fmaf(w[2], h[2 * r2 + 1], o0);
+                            o1 = __builtin_fmaf(w[3], h[2 * r2 + 1], o1);
+                        }
+                    }
+                    const int32_t oa = act_to_int(rintf(o0 * p.act_scale));  // drl_engine.py:38-39
+                    const int32_t ob = act_to_int(rintf(o1 * p.act_scale));
+                    const StepOut so1 = ftp_step(p, inv_min + si, oa, ob, tmid, task, tbid, tbmax, tsmin);
+                    to_s[si][lane] = (uint8_t)((si + so1.fill_buy - so1.fill_sell) | ((so1.fill_buy | so1.fill_sell) << 7));
+                    rl_s[si][lane] = so1.reward;
+                    __syncthreads();
+                    if (wv == 0) {
+                        // the chunk's steps from K on: segmented map scan, then each tracked
+                        // start's path from its state at K
+                        uint64_t map = kIdentityMap;
+                        uint32_t traded = 0;
+                        if (valid) {
+                            for (int st = 0; st < nsi; ++st) {
+                                const uint32_t b8 = to_s[st][lane];
+                                map = (map & ~(0xFFull << (8 * st))) | ((uint64_t)(b8 & 0x7Fu) << (8 * st));
+                                traded |= (b8 >> 7) << st;
+                            }
+                        }
+                        uint64_t inc = m_scan_seg(map, SEG);
+                        uint64_t excl = shfl_up_u64(inc, 1);
+                        const int u = lane & (SEG - 1);
+                        if (u == 0) excl = kIdentityMap;
+                        const int c = cg * kFrontierLanes + lg;
+                        const bool has = c < nch;
+                        const int64_t ci = frontier_rec(e, ep.ngrp, has ? c : 0);
+                        const uint64_t cur = args.cmaps[ci];
+                        const uint32_t ki = args.kinfo[ci];
+                        const bool merged = (int)(ki & kKinfoTick) < CL;
+                        const uint32_t p0 = ki >> 29;
+                        const uint32_t all = (1u << nsi) - 1u;
+                        const uint32_t sset = c == 0 ? 1u << (uint32_t)(-inv_min) : all;
+                        const int sh = (lane >> shs) << shs;
+                        const uint64_t segm = SEG == 64 ? ~0ull : (((1ull << SEG) - 1ull) << sh);
+                        // the last valid tick of the chunk: R_c - 1 (<= SEG - 1)
+                        const int ntl = has ? min(T, (c + 1) * CL) - c * CL : 0;
+                        const bool last = valid && u == ntl - K - 1;
+                        uint64_t cm = cur;
+#pragma unroll
+                        for (int st = 0; st < NSI; ++st) {
+                            const bool tr = st < nsi && ((sset >> st) & 1u);
+                            const uint32_t x = map_get(cur, (uint32_t)st);
+                            const uint32_t y = map_get(excl, x & 7u);
+                            if (valid && tr && (!merged || (uint32_t)st == p0))
+                                args.rew[(int64_t)st * ep.rs + rbase + frontier_row(K + u, lg)] = rl_s[y & 7u][lane];
+                            const uint32_t cnt = (uint32_t)__popcll(__ballot(valid && tr && ((traded >> (y & 7u)) & 1u)) & segm);
+                            if (last && tr) {
+                                args.ctr32[ci * 8 + st] += cnt;
+                                cm = (cm & ~(0xFFull << (8 * st))) | ((uint64_t)map_get(inc, x & 7u) << (8 * st));
+                            }
+                        }
+                        if (last) args.cmaps[ci] = cm;
+                    }
+                    __syncthreads();  // to_s / rl_s / hb_s are rewritten by the next pass
+                }
+            }
+            __syncthreads();  // list_s is rewritten by the next window
+        }
+    }
+}
+
+int launch_frontier_spill(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa) {
+    if (!fa.spill_budget || !fa.wspill || n_waves == 0) return SGMM_OK;
+    const int total = (int)(n_waves * (unsigned)ls);
+    const dim3 grid(kSpillBlocks), block(kWave * nsi);
+    if (hidden == 16) {
+        if (nsi <= 5) SGMM_LAUNCH((k_frontier_spill<16, 5>), grid, block, 0, s, fa, total, ls);
+        else SGMM_LAUNCH((k_frontier_spill<16, 8>), grid, block, 0, s, fa, total, ls);
+    } else {
+        if (nsi <= 5) SGMM_LAUNCH((k_frontier_spill<32, 5>), grid, block, 0, s, fa, total, ls);
+        else SGMM_LAUNCH((k_frontier_spill<32, 8>), grid, block, 0, s, fa, total, ls);
+    }
+    SGMM_LAUNCHED();
+    return SGMM_OK;
 }
 
 int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa) {

@@ -70,4 +70,8 @@ struct ProfScope {
 
 inline bool supported_hidden(int h) { return h == 8 || h == 16 || h == 32 || h == 64; }
 
+// Launch-plan override of knob k (SGMM_PLAN_*), or -1 for the default rule
+// (sgmm_plan_set; the -DSGMM_EXPERIMENTS build seeds them from SGMM_* variables)
+int32_t plan_value(int k);
+
 }  // namespace sgmm

@@ -223,11 +223,32 @@ struct FrontierArgs {
     uint32_t* kinfo;
     double* rew;
     uint32_t* wslots;  // one wave per walk: [e * ngrp + cg] = the MLP slots it ran (walk-order feedback), or null
+    // spill (k_frontier_spill): wave b of the launch writes wspill[b] = the tick
+    // offset at which it stopped (a multiple of 4, > 0), or 0 when it walked to
+    // the end; a walk stops once its MLP slots pass spill_budget (0: never) and
+    // its chunks have at most kSpillTicks ticks left
+    uint32_t* wspill;
+    uint32_t spill_budget;
 };
+constexpr int kSpillTicks = 64;  // a spilled chunk's remaining ticks fit one wave (lane = tick)
+
+// wave_map_scan within segments of SEG = 16, 32 or 64 lanes
+template <int SEG>
+__device__ __forceinline__ uint64_t wave_map_scan_seg(uint64_t m) {
+#define SGMM_MSTEP(CTRL, RM) m = map_then(dpp64<CTRL, RM>(kIdentityMap, m), m);
+    SGMM_MSTEP(0x111, 0xF) SGMM_MSTEP(0x112, 0xF) SGMM_MSTEP(0x114, 0xF) SGMM_MSTEP(0x118, 0xF)
+    if constexpr (SEG >= 32) { SGMM_MSTEP(0x142, 0xA) }
+    if constexpr (SEG >= 64) { SGMM_MSTEP(0x143, 0xC) }
+#undef SGMM_MSTEP
+    return m;
+}
 
 // launches the frontier kernel for hidden = 16 / 32 and nsi inventory states
 // (sgmm_frontier.hip): grid = episodes x ep.ngrp waves
 // ls: waves per 64-chunk group (1, 2 or 4; the grid is n_waves x ls)
 int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa);
+// completes the chunks of the walks that spilled (fa.wspill) tick-parallel; a
+// fixed grid (graph-capturable) that exits at once when no walk spilled
+int launch_frontier_spill(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa);
 
 }  // namespace sgmm

@@ -36,6 +36,7 @@
 // implementation; the tests require both paths to agree bit for bit).
 #include <algorithm>
 #include <climits>
+#include <atomic>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -2059,17 +2060,23 @@ static int check_episodes(const sgmm_ticks* tk, const sgmm_episodes* eps, const 
 // launch has fewer than two walks per SIMD the episodes are cut into 2-4
 // groups of 64 chunks of proportionally fewer ticks;
 // each extra group pays for tracking every start state of its chunks until
-// their paths merge.  SGMM_FRONTIER_NW=1..16 forces the count (records and
+// their paths merge.  SGMM_PLAN_GROUPS = 1..16 forces the count (records and
 // plane padding are laid out for the launch's count, frontier_rec / frontier_pad).
 constexpr int kFrontierAutoWaves = 8;  // the default rule's cap
+// SIMDs of the current device (cached per device id; 256 CUs if the query fails)
 static int simd_count() {
-    static int n = 0;
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> cache[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    std::atomic<int>& c = cache[dev < kMaxDev ? dev : kMaxDev - 1];
+    int n = c.load(std::memory_order_relaxed);
     if (n == 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
         n = 4 * cus;
+        c.store(n, std::memory_order_relaxed);
     }
     return n;
 }
@@ -2082,12 +2089,10 @@ struct FrontierPlan {
 };
 static FrontierPlan frontier_plan(int32_t n) {
     FrontierPlan p{1, 1, std::max(n, 0), 1, std::max<int64_t>(n, 0), 1};
-    if (const char* v = std::getenv("SGMM_FRONTIER_LS")) {  // experiments: waves per walk
-        const int l = std::atoi(v);
-        if (l == 2 || l == 4) p.ls = l;
-    }
-    if (const char* v = std::getenv("SGMM_FRONTIER_NW")) {
-        const int g = std::atoi(v);
+    const int ls_force = plan_value(SGMM_PLAN_LANE_SPLIT);  // tests / experiments: waves per walk
+    if (ls_force == 2 || ls_force == 4) p.ls = ls_force;
+    {
+        const int g = plan_value(SGMM_PLAN_GROUPS);
         if (g >= 1 && g <= kFrontierMaxWaves) {
             p.g0 = p.gtail = p.gmax = g;
             p.waves = (int64_t)n * g;
@@ -2105,7 +2110,7 @@ static FrontierPlan frontier_plan(int32_t n) {
     // four waves per SIMD without more chunk starts (the 1-of-16 shard, 512
     // episodes: frontier + scan 248.5 us at G = 4 with two waves per walk against
     // 255.9 us at G = 8 and 270.6 us at G = 4 with one, profiles/r05_small/ls_*, c5s16_fr4)
-    if (n <= S / 2 && p.ls == 1 && !std::getenv("SGMM_FRONTIER_LS")) p.ls = 2;
+    if (n <= S / 2 && ls_force < 0) p.ls = 2;
     // Whole walks are dispatched one per SIMD per run of S waves, so n = a S + r
     // leaves r SIMDs with a walk more than the others, and the walks on those
     // SIMDs end last.  The r episodes at the end of the order are cut into
@@ -2113,14 +2118,10 @@ static FrontierPlan frontier_plan(int32_t n) {
     // one per SIMD (1536 = 1024 + 512 -> 1024 whole walks and 512 episodes in 2
     // groups; config 3's 2560 = 2 x 1024 + 512 -> 2048 + 512 in 2 groups took
     // the policy kernel from 547 to 525 us, before the four-walk rule below).
-    // SGMM_FRONTIER_TAIL=0 keeps every walk whole.
-    static const bool tail = [] {
-        const char* v = std::getenv("SGMM_FRONTIER_TAIL");
-        return !(v && std::strcmp(v, "0") == 0);
-    }();
+    // SGMM_PLAN_TAIL = 0 keeps every walk whole.
+    const bool tail = plan_value(SGMM_PLAN_TAIL) != 0;
     const int64_t r = n % S;
-    const char* fw = std::getenv("SGMM_FRONTIER_FOUR");  // experiments: 0 = no four-walk rule
-    const bool four = !(fw && std::strcmp(fw, "0") == 0);
+    const bool four = plan_value(SGMM_PLAN_FOUR) != 0;  // experiments: 0 = no four-walk rule
     if (tail && four && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
         // from 2.5 episodes per SIMD up to 4: four walks per SIMD, 2n - 4S whole
         // and the rest in halves, one whole and three half walks per SIMD (config
@@ -2142,6 +2143,19 @@ static FrontierPlan frontier_plan(int32_t n) {
 // the record / plane-padding layout of a launch of n episodes
 static int32_t frontier_groups(int32_t n) { return frontier_plan(n).gmax; }
 
+// Spill budget of a frontier launch in MLP slots per walk: SGMM_PLAN_SPILL / 16
+// slots per tick of the launch's longest walk (its g0-group chunks), 0 = no
+// spill.  A walk stops once past it and its chunks have <= kSpillTicks ticks
+// left; k_frontier_spill runs the rest tick-parallel.
+constexpr int kSpillDefault = 0;
+static uint32_t spill_budget(const sgmm_episodes* eps, const FrontierPlan& plan) {
+    int v = plan_value(SGMM_PLAN_SPILL);
+    if (v < 0) v = kSpillDefault;
+    if (v == 0 || eps->max_len <= 0) return 0;
+    const int64_t cl = frontier_len(eps->max_len, plan.g0);
+    return (uint32_t)std::max<int64_t>(1, (int64_t)v * cl / 16);
+}
+
 
 // plane stride: every tick, plus (no adversary: the frontier kernel may run)
 // the frontier layout's padding rows per episode, frontier_pad(G) with G the
@@ -2158,14 +2172,11 @@ static EpArrays ep_arrays(const sgmm_episodes* e, bool with_adv) {
 
 static size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// Policy kernel selection, SGMM_TABLE_PATH: unset = the default (frontier
-// kernel for many episodes, else the f32-MFMA table); "frontier" / "table"
-// force either; "valu" forces the VALU table (one lane per (tick, state)), an
-// independent cross-check in the tests.
-static bool table_valu() {
-    const char* e = std::getenv("SGMM_TABLE_PATH");
-    return e && std::strcmp(e, "valu") == 0;
-}
+// Policy kernel selection, SGMM_PLAN_POLICY_PATH: default = the frontier
+// kernel for many episodes, else the f32-MFMA table; 1 / 2 force either; 3
+// forces the VALU table (one lane per (tick, state)), an independent
+// cross-check in the tests.
+static bool table_valu() { return plan_value(SGMM_PLAN_POLICY_PATH) == 3; }
 
 }  // namespace sgmm
 
@@ -2188,7 +2199,7 @@ extern "C" int sgmm_debug_tstamps(unsigned long long* host, int n_waves) {
 
 // Workspace layout (256-byte aligned sections), per batch of total_steps ticks:
 //   no adversary: u64 cmaps[nc] | u64 ctr[nc] (nc = total_steps/64 + n + 1 chunk
-//                 slots) | u32 kinfo[n * 64 G] | u32 wslots[n * 64] | f64 path planes
+//                 slots) | u32 kinfo[n * 64 G] | u32 wslots[n * 64] | u32 wspill[n * 64] | f64 path planes
 //                 rew[n_states][rs] (rs = total_steps + frontier_pad(G) n,
 //                 rounded up to 32; G = frontier_groups(n))
 //   adversary:    u64 fills[total_steps] | f64 rew[n_states][rs] (rs =
@@ -2209,6 +2220,9 @@ static size_t ws_kinfo(int32_t n) { return align256(n_frontier_slots(n) * sizeof
 static size_t ws_fills(int64_t steps) { return align256((size_t)steps * sizeof(uint64_t)); }
 // u32 wslots[n * 64]: the frontier launch's MLP slots per walk, [e * G + group] (G <= 16)
 static size_t ws_wslots(int32_t n) { return align256((size_t)n * 64 * sizeof(uint32_t)); }
+// u32 wspill[n * 64]: per frontier wave (<= 16 groups x 4 waves per episode) the
+// tick offset at which it spilled, 0 if it did not
+static size_t ws_wspill(int32_t n) { return align256((size_t)n * 64 * sizeof(uint32_t)); }
 
 // The workspace of a batch with n_inventory inventory values, with or
 // without the adversary (then 4 * n_inventory states: inventory x previous
@@ -2219,7 +2233,8 @@ static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t 
     if (arl)  // fill codes, per-state planes rew[state * rs + row]
         return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes, true) * (size_t)(4 * nsi) * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           ws_wslots(n_episodes) + (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
+           ws_wslots(n_episodes) + ws_wspill(n_episodes) +
+           (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
 }
 
 extern "C" size_t sgmm_rollout_workspace_bytes(int32_t n_episodes, int64_t total_steps, int32_t n_inventory,
@@ -2239,8 +2254,8 @@ extern "C" size_t sgmm_rollout_workspace_size(int32_t n_episodes, int64_t total_
 // Frontier kernel or table: the frontier kernel does ~1/3 of the table's
 // matrix work but walks each episode serially (one wave per episode), so it
 // needs many episodes to fill the chip; it is also the only path for episodes
-// longer than kMaxLen.  SGMM_TABLE_PATH=frontier / table forces either,
-// SGMM_FRONTIER_MIN_EPS moves the threshold.  Measured crossover (one rank's
+// longer than kMaxLen.  SGMM_PLAN_POLICY_PATH forces either,
+// SGMM_PLAN_MIN_EPS moves the threshold.  Measured crossover (one rank's
 // shard of config 5, H = 32, 3600 ticks, per generation, profiles/r03_c5_shard*):
 // 256 episodes table 235 / frontier 363 us, 512: 365 / 435, 1024: 633 / 525,
 // 2048: 1078 / 572 -- the lines crossed near 700 episodes.  With 2-4 chunk
@@ -2250,21 +2265,18 @@ constexpr int kFrontierMinEps = 512;
 static bool use_frontier(bool arl, int hidden, const sgmm_episodes* eps) {
     if (arl || (hidden != 16 && hidden != 32)) return false;
     if (eps->max_len > kMaxLen) return true;
-    const char* v = std::getenv("SGMM_TABLE_PATH");
-    if (v && std::strcmp(v, "frontier") == 0) return true;
-    if (v && *v) return false;
-    static const int min_eps = [] {
-        const char* m = std::getenv("SGMM_FRONTIER_MIN_EPS");
-        return m && std::atoi(m) > 0 ? std::atoi(m) : kFrontierMinEps;
-    }();
-    return eps->n >= min_eps;
+    const int path = plan_value(SGMM_PLAN_POLICY_PATH);
+    if (path == 1) return true;
+    if (path > 1) return false;
+    const int m = plan_value(SGMM_PLAN_MIN_EPS);
+    return eps->n >= (m > 0 ? m : kFrontierMinEps);
 }
 
 // The one-state-per-wave table for launches of at most kTableSpChunks chunks
-// (SGMM_TABLE_SP=0 / 1 forces v3 / it, for A/B and the tests)
+// (SGMM_PLAN_TABLE_SP = 0 / 1 forces v3 / it, for A/B and the tests)
 constexpr int64_t kTableSpChunks = 256;
 static bool table_sp(int nch, int n_ep) {
-    if (const char* v = std::getenv("SGMM_TABLE_SP")) return std::atoi(v) != 0;
+    if (const int v = plan_value(SGMM_PLAN_TABLE_SP); v >= 0) return v != 0;
     return (int64_t)nch * n_ep <= kTableSpChunks;
 }
 
@@ -2344,8 +2356,8 @@ extern "C" int sgmm_ordered_sum(const double* values, int64_t n, double init, do
 // path-scan workgroup size for n episodes (256 CUs): one 16-wave workgroup per
 // CU while they fit, then 8-wave, then 4-wave workgroups
 static int scan_threads(int64_t n) {
-    if (const char* v = std::getenv("SGMM_SCAN_THREADS")) {
-        const int t = std::atoi(v);
+    {
+        const int t = plan_value(SGMM_PLAN_SCAN_THREADS);
         if (t == 64 || t == 256 || t == 512 || t == 1024) return t;
     }
     // beyond 512 episodes one-wave workgroups: the exact-sum walk is serial,
@@ -2375,24 +2387,27 @@ static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const
 }
 
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
-// per walk, whole populations of equal-length episodes, a caller's order array
-static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, const GenomeSrc& src) {
-    const char* v = std::getenv("SGMM_FRONTIER_REORDER");
-    const bool on = !(v && std::strcmp(v, "0") == 0);
+// per walk, whole populations of equal-length episodes, the caller's writable
+// walk order (sgmm_populations::walk_order)
+static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, const GenomeSrc& src,
+                         const int32_t* walk_order) {
     const int P = src.pop_eps;
-    return on && eps->order && P > 0 && eps->n % P == 0 && eps->n / P >= 2 && eps->n / P <= kReorderMaxPops &&
+    return walk_order && eps->order == walk_order && P > 0 && eps->n % P == 0 && eps->n / P >= 2 &&
+           eps->n / P <= kReorderMaxPops &&
            plan.ls == 1 && plan.g0 == 1 && plan.gtail == 2 && plan.whole > 0 && plan.whole < eps->n &&
            eps->total_steps == (int64_t)eps->n * eps->max_len;
 }
 
 // table + path scan (+ the generation tail when step.st) for one batch
-// rj_out: a training launch with the walk-order feedback hands its job here
-// instead of launching it; rj_in: a job to run inside (or after) this launch
+// walk_order: the caller's writable walk order (eps->order points at it) for the
+// walk-order feedback; rj_out: a training launch with the feedback hands its job
+// here instead of launching it; rj_in: a job to run inside (or before) this launch
 static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                         const sgmm_env_params* params, const GenomeSrc& src, bool arl,
                         int32_t hidden, double* fitness, int32_t* trades, void* workspace,
                         size_t workspace_bytes, const StepArgs& step, hipStream_t s,
-                        ReorderJob* rj_out = nullptr, const ReorderJob* rj_in = nullptr) {
+                        ReorderJob* rj_out = nullptr, const ReorderJob* rj_in = nullptr,
+                        int32_t* walk_order = nullptr) {
     SGMM_REQUIRE(fitness && trades, "null fitness/trades output");
     if (eps->n == 0) return SGMM_OK;
     const int32_t nsi = eps->inv_max - eps->inv_min + 1;
@@ -2408,6 +2423,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     uint64_t* fills = nullptr;
     uint32_t* kinfo = nullptr;
     uint32_t* wslots = nullptr;
+    uint32_t* wspill = nullptr;
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
@@ -2418,7 +2434,8 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ctr = reinterpret_cast<uint64_t*>(w + a);
         kinfo = reinterpret_cast<uint32_t*>(w + a + b);
         wslots = reinterpret_cast<uint32_t*>(w + a + b + ws_kinfo(eps->n));
-        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n));
+        wspill = reinterpret_cast<uint32_t*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n));
+        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n) + ws_wspill(eps->n));
     }
     EpArrays ep = ep_arrays(eps, arl);
     const ReorderJob* rj_fold = nullptr;
@@ -2437,28 +2454,49 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                  kMaxLen);
     SGMM_REQUIRE(!fr || eps->max_len <= kFrontierMaxLen, "max_len=%d > %lld ticks per episode",
                  eps->max_len, (long long)kFrontierMaxLen);
+    if (rj_in && rj_in->order) {
+        // a walk-order job rides along in this launch's state-parallel table when it takes
+        // that path and its workspace use ends below the job's slot counts; otherwise it
+        // runs first, before this launch can touch the workspace
+        const int nch = (eps->max_len + kChunk - 1) / kChunk;
+        const bool fold = !fr && !arl && eps->max_len > 0 && (hidden == 16 || hidden == 32) && !table_valu() &&
+                          table_sp(nch, eps->n) &&
+                          reinterpret_cast<const char*>(rj_in->wslots) >= w + rollout_ws_bytes(eps->n, eps->total_steps, nsi, arl);
+        if (fold) {
+            rj_fold = rj_in;
+        } else {
+            SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, *rj_in);
+            SGMM_LAUNCHED();
+            rj_done = true;
+        }
+    }
     if (fr && eps->max_len > 0) {
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
         const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
-                              kinfo, rew, wslots};
+                              kinfo, rew, wslots, wspill, spill_budget(eps, plan)};
         if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, plan.ls, s, fa)) return rc;
+        if (fa.spill_budget) {
+            ProfScope prof2(vt ? "val_frontier_spill" : "frontier_spill", s);
+            if (int rc = launch_frontier_spill(hidden, nsi, (unsigned)plan.waves, plan.ls, s, fa)) return rc;
+        }
     } else if (eps->max_len > 0) {
         dim3 grid((eps->max_len + kChunk - 1) / kChunk, eps->n);
         ProfScope prof(vt ? "val_policy_table" : "policy_table", s);
         const bool valu = table_valu();
-        // the job may ride along only if this launch's workspace use ends below its slot counts
-        if (rj_in && rj_in->order &&
-            reinterpret_cast<const char*>(rj_in->wslots) >= w + rollout_ws_bytes(eps->n, eps->total_steps, nsi, arl))
-            rj_fold = rj_in;
-        switch (hidden) {
+        if (rj_fold) {  // the walk-order job rides along in the state-parallel table
+            if (hidden == 16)
+                launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
+            else
+                launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
+        } else switch (hidden) {
             case 8: launch_table<8>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew); break;
             case 16:
                 if (valu) launch_table<16>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
-                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
+                else launch_table_mfma<16>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
                 break;
             case 32:
                 if (valu) launch_table<32>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
-                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew, rj_fold, &rj_done);
+                else launch_table_mfma<32>(arl, nsi, eps->max_len, eps->n, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
                 break;
             default:
                 if (valu) launch_table<64>(arl, nsi, grid, s, *ticks, ep, params, src, eps->inv_min, ctr, cmaps, fills, rew);
@@ -2506,14 +2544,11 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         }
     }
     SGMM_LAUNCHED();
-    if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src)) {
-        ReorderJob job{wslots, const_cast<int32_t*>(eps->order), eps->n, plan.whole, plan.gtail, src.pop_eps};
-        if (const char* v = std::getenv("SGMM_REORDER_WEIGHTS")) {
-            unsigned a = 0, b = 0;
-            if (std::sscanf(v, "%u,%u", &a, &b) == 2 && a > 0 && b > 0 && a < 64 && b < 64) {
-                job.w_whole = a;
-                job.w_split = b;
-            }
+    if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src, walk_order)) {
+        ReorderJob job{wslots, walk_order, eps->n, plan.whole, plan.gtail, src.pop_eps};
+        if (const int w = plan_value(SGMM_PLAN_REORDER_WEIGHTS); w > 0 && (w >> 8) > 0 && (w & 255) > 0) {
+            job.w_whole = (uint32_t)(w >> 8) & 63u;
+            job.w_split = (uint32_t)w & 63u;
         }
         if (rj_out) {
             *rj_out = job;
@@ -2522,9 +2557,9 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
             SGMM_LAUNCHED();
         }
     }
-    if (rj_in && rj_in->order && !rj_done) {  // the job did not ride along: on its own
-        SGMM_LAUNCH(k_walk_reorder, dim3(1), dim3(kScanThreads), 0, s, *rj_in);
-        SGMM_LAUNCHED();
+    if (rj_in && rj_in->order && !rj_done) {  // (not reached: a job that cannot ride along ran first)
+        set_error("walk-order job neither folded nor launched");
+        return SGMM_ERR_ARG;
     }
     return SGMM_OK;
 }
@@ -2679,10 +2714,24 @@ extern "C" int sgmm_generation_multi_best(const sgmm_ticks* ticks, const sgmm_ep
     src.adv_pstride = n_adv;
     StepArgs step{pops->states, pops->masters_mm, pops->masters_adv, pops->best_masters, n_mm, n_adv, 0,
                   pops->history, pops->history_cap, P, P, pops->seeds, 3};
+    // the validation batch is checked before anything is enqueued
+    if (int rc = check_episodes(ticks, val_eps, params, pops->masters_mm, H)) return rc;
+    {
+        const int32_t vnsi = val_eps->inv_max - val_eps->inv_min + 1;
+        const size_t vneed = rollout_ws_bytes(val_eps->n, val_eps->total_steps, vnsi, false);
+        if (val_eps->n > 0 && (!workspace || workspace_bytes < vneed)) {
+            set_error("workspace %zu bytes < required %zu (validation batch)", workspace_bytes, vneed);
+            return SGMM_ERR_WORKSPACE;
+        }
+    }
     hipStream_t s = as_stream(stream);
     ReorderJob job{nullptr, nullptr, 0, 0, 0, 1};
-    if (int rc = rollout_impl(ticks, train_eps, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
-                              step, s, &job))
+    // the training launch walks the caller's writable walk order when given
+    // (the feedback rewrites it); train_eps itself is only read
+    sgmm_episodes tr = *train_eps;
+    if (pops->walk_order) tr.order = pops->walk_order;
+    if (int rc = rollout_impl(ticks, &tr, params, src, arl, H, fitness, trades, workspace, workspace_bytes,
+                              step, s, &job, nullptr, pops->walk_order))
         return rc;
     return validate_impl(ticks, val_eps, params, pops, val_fitness, val_trades, workspace, workspace_bytes, s, true,
                          &job);

@@ -158,12 +158,17 @@ class DRLEngine:
       exchange    -- "auto": shard + all-gather only with several ranks; "always":
                      take the sharded path (asked rollout, all-gather, GA step) on
                      one process too -- the multi-GPU path rehearsed on one GPU.
+      walk_feedback -- True: the session owns a device walk order that the library
+                     rewrites after each training launch (sgmm_populations::walk_order:
+                     the lightest populations are walked whole next generation);
+                     scheduling only, results do not depend on it.
     """
 
     def __init__(self, pop_size=50, sigma=0.05, phi=0.01, tick_size=0.01, fee_rate=0.0,
                  use_arl=False, save_dir="checkpoints/drl", *, hidden_dim=32, rng="device",
                  seed=None, val_mode="auto", honor_sigma=False, sync_every=10, dist=None,
-                 device=None, verbose=True, patience=15, decay=0.5, use_graph=True, exchange="auto"):
+                 device=None, verbose=True, patience=15, decay=0.5, use_graph=True, exchange="auto",
+                 walk_feedback=True):
         self.phi = phi
         self.tick_size = tick_size
         self.fee_rate = fee_rate
@@ -197,6 +202,7 @@ class DRLEngine:
         if exchange not in ("auto", "always"):
             raise ValueError("exchange must be 'auto' or 'always'")
         self.exchange = exchange
+        self.walk_feedback = bool(walk_feedback)
         self.timing = {}
 
     def _log(self, msg):
@@ -408,9 +414,13 @@ class TrainingSession(_GraphedGenerations):
         self.asked = AskedPopulation(self.state.data_ptr(), self.master.data_ptr(),
                                      self.master_adv.data_ptr() if arl else None, eng.seed, self.i0, 0)
         self.seeds = torch.tensor([int(eng.seed)], dtype=torch.int64).to(dev)
+        # the frontier kernel's walk order, rewritten on the device by the walk-order
+        # feedback (sgmm_populations::walk_order); train_eps stays read-only
+        self.walk_order = self.train_eps.dev["order"].clone()
         self.pops = _lib.Populations(1, P, H, self.generations, self.state.data_ptr(), self.master.data_ptr(),
                                      self.master_adv.data_ptr() if arl else None, self.best_master.data_ptr(),
-                                     self.seeds.data_ptr(), self.hist.data_ptr())
+                                     self.seeds.data_ptr(), self.hist.data_ptr(),
+                                     self.walk_order.data_ptr() if eng.walk_feedback else None)
         # one generation = fixed launches -> replayable HIP graphs: the whole
         # generation on one rank; with several ranks the rollout and the boundary
         # are captured separately around the (eager) all-gather
@@ -734,9 +744,13 @@ class MultiSession(_GraphedGenerations):
                 raise ValueError("mm and adversary sigma must start equal (one device state holds both)")
             check(self.L.sgmm_ga_state_init(ctypes.c_void_p(self.states[k].data_ptr()), float(e.mm_evolver.sigma),
                                             e.patience, e.decay, stream_ptr()), "sgmm_ga_state_init")
+        # the frontier kernel's walk order, rewritten on the device by the walk-order
+        # feedback (sgmm_populations::walk_order); the episode batch stays read-only
+        self.walk_order = self.eps.dev["order"].clone()
         self.pops = _lib.Populations(K, P, H, self.generations, self.states.data_ptr(), self.masters.data_ptr(),
                                      self.masters_adv.data_ptr() if arl else None, self.best_masters.data_ptr(),
-                                     self.seeds.data_ptr(), self.hist.data_ptr())
+                                     self.seeds.data_ptr(), self.hist.data_ptr(),
+                                     self.walk_order.data_ptr() if e0.walk_feedback else None)
         self.use_graph = bool(e0.use_graph)
         self.graphs, self.batch_graph, self.batch_graphs, self.full_graph = None, None, {}, False
         self.graph_batch = max(1, min(self.GRAPH_BATCH, e0.sync_every))

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SGMM_ABI_VERSION 4
+#define SGMM_ABI_VERSION 5
 
 enum {
     SGMM_OK = 0,
@@ -309,7 +309,16 @@ typedef struct sgmm_populations {
     float *best_masters;        /* [K][H*H+7H+2] checkpoint slots (drl_engine.py:144-150) */
     const uint64_t *seeds;      /* [K] device: per-population Philox key */
     sgmm_ga_history *history;   /* [K][history_cap] */
-} sgmm_populations;             /* 64 bytes */
+    /* (ABI 5) optional, may be NULL: [K*P] device, the frontier kernel's walk
+     * order of the TRAINING episodes for sgmm_generation_multi_best, read and
+     * REWRITTEN on the device after each training launch (the walk-order
+     * feedback; scheduling only, results do not depend on it).  The caller
+     * seeds it with a permutation (e.g. a copy of train_eps->order), owns it
+     * for the session and must not share it between concurrent calls.  NULL:
+     * no feedback, train_eps->order is only read.  Every other entry point
+     * ignores it.  The library never writes any sgmm_episodes array. */
+    int32_t *walk_order;
+} sgmm_populations;             /* 72 bytes */
 
 /* One generation of K populations on one process.  Episodes: population k
  * owns episodes [2Pk, 2Pk+P) (training, individual genome[e]) and
@@ -342,12 +351,13 @@ int sgmm_rollout_fitness_asked_multi(const sgmm_ticks *ticks, const sgmm_episode
  * fitness/trades [K*P] (training), val_fitness/val_trades [K].  The workspace
  * must hold the larger of the two batches: sgmm_rollout_workspace_bytes(n,
  * steps, n_inventory, with_adversary) of each, with_adversary = masters_adv !=
- * NULL for the training batch and 0 for the validation batch.  When the
+ * NULL for the training batch and 0 for the validation batch.  With
+ * pops->walk_order set, the training launch walks in that order and, when the
  * frontier kernel cuts some training episodes into halves (2.5-4 episodes per
- * SIMD) and the populations' episodes are of equal length, train_eps->order is
- * rewritten on the device after the training launch so the next generation
- * walks the lightest populations whole (scheduling only: results do not depend
- * on the order; SGMM_FRONTIER_REORDER=0 disables it). */
+ * SIMD) and the populations' episodes are of equal length, rewrites it on the
+ * device after the launch so the next generation walks the lightest
+ * populations whole (scheduling only: results do not depend on the order).
+ * train_eps is read-only. */
 int sgmm_generation_multi_best(const sgmm_ticks *ticks, const sgmm_episodes *train_eps,
                                const sgmm_episodes *val_eps, const sgmm_env_params *params,
                                const sgmm_populations *pops, double *fitness, int32_t *trades,
@@ -458,6 +468,35 @@ int sgmm_step_bundle(const sgmm_event_bars *ev, int32_t n_days, const int64_t *s
 int sgmm_sgu2_forward(const float *weights, int32_t hidden, const float *X, int64_t n,
                       int32_t time_steps, const float *mean, const float *std, float *out,
                       void *stream);
+
+/* ------------------------------------------------------------------------
+ * Launch-plan overrides (ABI 5), for tests and A/B experiments.  The shipped
+ * library reads no environment variable; its launch plan (policy kernel,
+ * chunk groups, lane split, scan width, spill budget) follows the measured
+ * rules documented in DESIGN.md unless overridden here.  Overrides are
+ * process-wide and apply to launches ENQUEUED after the call (a captured HIP
+ * graph keeps the plan it was captured with); set them before building
+ * workspaces, since the workspace size follows the plan.  value < 0 restores
+ * the default rule.  sgmm_plan_set returns 0 or SGMM_ERR_ARG (unknown knob);
+ * sgmm_plan_get returns the override, -1 for the default rule, or INT32_MIN for
+ * an unknown knob.  (A build with -DSGMM_EXPERIMENTS also takes the initial
+ * values from the SGMM_* environment variables named in DESIGN.md.)
+ * ------------------------------------------------------------------------ */
+enum {
+    SGMM_PLAN_POLICY_PATH = 0,   /* 0 auto, 1 frontier, 2 MFMA table, 3 VALU table */
+    SGMM_PLAN_GROUPS = 1,        /* frontier chunk groups per episode, 1..16 */
+    SGMM_PLAN_LANE_SPLIT = 2,    /* frontier waves per walk: 1, 2 or 4 */
+    SGMM_PLAN_TAIL = 3,          /* 0: no split tail walks (every walk whole) */
+    SGMM_PLAN_FOUR = 4,          /* 0: no four-walk rule */
+    SGMM_PLAN_MIN_EPS = 5,       /* frontier kernel from this many episodes */
+    SGMM_PLAN_TABLE_SP = 6,      /* 0 / 1: state-parallel table off / forced */
+    SGMM_PLAN_SCAN_THREADS = 7,  /* path-scan workgroup: 64, 256, 512 or 1024 */
+    SGMM_PLAN_REORDER_WEIGHTS = 8, /* walk-order scores: whole << 8 | split */
+    SGMM_PLAN_SPILL = 9,         /* frontier spill budget, MLP slots per walk tick x 16 (0: off) */
+    SGMM_PLAN_N = 10
+};
+int sgmm_plan_set(int32_t knob, int32_t value);
+int sgmm_plan_get(int32_t knob);
 
 /* Kernel timing for benchmarks / diagnostics (not on by default).
  * While enabled, every kernel the library launches is bracketed by a pair of

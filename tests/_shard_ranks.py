@@ -112,12 +112,13 @@ def multi_train_rank(rank, world, port, P, gens, outdir, val_mode, arl, table_pa
     the K records, then the multi-population tell/validation (best) or GA
     step (fused) on the gathered records -- the cross-rank record addressing
     (i / n) * K * record + k * stride + (i % n) * size with i / n > 0."""
-    if table_path:
-        os.environ["SGMM_TABLE_PATH"] = table_path
     dist = _setup(rank, world, port)
     try:
         import sgmm_pkg
         sg = sgmm_pkg.load()
+        if table_path:
+            from sgmm_amd import _lib
+            _lib.plan_set(policy_path=table_path)
         tr, va, st = multi_workload()
         multi = multi_engines(sg, P, arl, os.path.join(outdir, f"ck{rank}"), val_mode)
         sess = multi.session(tr, va, st, generations=gens)

@@ -93,3 +93,18 @@ def agree_until_justified_divergence(act_ours, act_ref, raw_ref, scale=5.0):
     t = int(diff[0])
     assert np.any(near_tie(raw_ref[t], scale)), (t, act_ours[t], act_ref[t], raw_ref[t])
     return t
+
+
+@pytest.fixture
+def plan(sgmm):
+    """Launch-plan overrides for one test (sgmm_plan_set: policy_path, groups,
+    lane_split, table_sp, spill, ...), restored to the default rules afterwards."""
+    from sgmm_amd import _lib
+    saved = {}
+
+    def set_(**knobs):
+        for k, v in _lib.plan_set(**knobs).items():
+            saved.setdefault(k, v)
+
+    yield set_
+    _lib.plan_set(**saved)

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(sgmm):
     assert declared <= exported, declared - exported
     assert exported <= declared, exported - declared  # nothing undocumented
     assert set(_lib.SIGNATURES) == declared            # the binding covers the header
-    assert L.sgmm_abi_version() == 4
+    assert L.sgmm_abi_version() == 5
 
 
 def test_struct_layouts_match_header(sgmm):
@@ -48,6 +48,10 @@ def test_struct_layouts_match_header(sgmm):
     assert _lib.GAState.arrivals.offset == 68
     assert ctypes.sizeof(_lib.DayStreams) == 104 and _lib.DayStreams.snap_off.offset == 16
     assert ctypes.sizeof(_lib.EventBars) == 88 and _lib.EventBars.vwap_num.offset == 80
+    # ABI 5: the writable walk order is its own member (train_eps->order stays read-only)
+    assert ctypes.sizeof(_lib.Populations) == 72 and _lib.Populations.walk_order.offset == 64
+    text = HEADER.read_text()
+    assert "const int32_t *order;" in text and "int32_t *walk_order;" in text
 
 
 def test_argument_errors_need_no_gpu(sgmm):
@@ -61,7 +65,7 @@ def test_argument_errors_need_no_gpu(sgmm):
     # H = 64 genomes (4546 floats) overflow the GA step's LDS master stage: rejected
     # before launch by every multi-population GA entry point
     v = ctypes.c_void_p(8)
-    pops = _lib.Populations(1, 8, 64, 0, 8, 8, None, None, 8, None)
+    pops = _lib.Populations(1, 8, 64, 0, 8, 8, None, None, 8, None, None)
     for rc in (L.sgmm_ga_step_multi(ctypes.byref(pops), v, v, v, v, 0, 0, 0, 0, None),
                L.sgmm_ga_tell_multi(ctypes.byref(pops), v, v, 0, 0, 0, 0, None)):
         assert rc == -1 and b"genome too large" in L.sgmm_last_error()
@@ -70,9 +74,10 @@ def test_argument_errors_need_no_gpu(sgmm):
     # frontier kernel (64 G chunk records per episode -- G = 8 groups of 64 chunks at 4
     # episodes, the default rule's cap: u64 map, u32[8] counts, u32 merge info) (planes:
     # 1000 ticks + 4 x (256 G + 16) padding rows of the frontier layout -- 128-byte aligned
-    # episode blocks -- rounded to 32: 9280); u32 slots per frontier wave (64 per episode)
+    # episode blocks -- rounded to 32: 9280); u32 slots per frontier wave (64 per episode);
+    # u32 spill entries per frontier wave (64 per episode: <= 16 groups x 4 waves)
     assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 512 * 8 + 4 * 512 * 32 + 4 * 512 * 4
-                                                         + 4 * 64 * 4 + 5 * 9280 * 8)
+                                                         + 4 * 64 * 4 + 4 * 64 * 4 + 5 * 9280 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)
@@ -105,3 +110,53 @@ def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError, match="no HIP device"):
         sgmm.RolloutEngine("cuda")
+
+
+PLAN_ENV = {"SGMM_TABLE_PATH": "frontier", "SGMM_FRONTIER_NW": "3", "SGMM_FRONTIER_LS": "2",
+            "SGMM_FRONTIER_TAIL": "0", "SGMM_FRONTIER_FOUR": "0", "SGMM_FRONTIER_MIN_EPS": "4",
+            "SGMM_TABLE_SP": "1", "SGMM_SCAN_THREADS": "256", "SGMM_REORDER_WEIGHTS": "5,5",
+            "SGMM_FRONTIER_SPILL": "0", "SGMM_FRONTIER_REORDER": "0"}
+
+
+def test_shipped_library_reads_no_plan_environment(sgmm):
+    """The shipped libsgmm.so takes its launch plan from the measured rules and
+    the explicit sgmm_plan_set overrides only: with every experiment variable of
+    the A/B builds set, each knob still reads -1 (the default rule) and the
+    workspace size is the default plan's; the variable names are not even in
+    the binary (they are compiled only into -DSGMM_EXPERIMENTS variants)."""
+    import os
+    import sys
+    from sgmm_amd import _lib
+    blob = _lib.LIB_PATH.read_bytes()
+    for name in PLAN_ENV:
+        assert name.encode() not in blob, name
+    assert b"getenv" not in blob
+    code = ("import sgmm_pkg; sgmm_pkg.load(); from sgmm_amd import _lib; L = _lib.load(); "
+            "print([L.sgmm_plan_get(k) for k in range(10)], L.sgmm_rollout_workspace_bytes(2560, 2560 * 4560, 5, 0), "
+            "L.sgmm_plan_get(10))")
+    env = dict(os.environ)
+    clean = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
+                           check=True).stdout.split("\n")[-2]
+    env.update(PLAN_ENV)
+    dirty = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
+                           check=True).stdout.split("\n")[-2]
+    assert dirty == clean
+    assert clean.startswith("[" + ", ".join(["-1"] * 10) + "]")
+    assert clean.endswith(str(-2**31))  # unknown knob
+
+
+def test_plan_overrides_round_trip(sgmm):
+    """sgmm_plan_set / sgmm_plan_get (no GPU needed): a knob reads back what was
+    set, a negative value restores the default rule, unknown knobs are
+    rejected; the workspace size follows a groups override (records and plane
+    padding are laid out for the launch's chunk groups)."""
+    from sgmm_amd import _lib
+    L = _lib.load()
+    base = L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0)
+    with _lib.plan(groups=16, policy_path="valu"):
+        assert L.sgmm_plan_get(_lib.PLAN_KNOBS["groups"]) == 16
+        assert L.sgmm_plan_get(_lib.PLAN_KNOBS["policy_path"]) == 3
+        assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) > base
+    assert L.sgmm_plan_get(_lib.PLAN_KNOBS["groups"]) == -1
+    assert L.sgmm_rollout_workspace_bytes(4, 1000, 5, 0) == base
+    assert L.sgmm_plan_set(99, 1) == -1 and b"unknown plan knob" in L.sgmm_last_error()

@@ -18,16 +18,26 @@ DEV = torch.device("cuda:0")
 
 
 @pytest.fixture(params=[1, 2, 3, 4, 8, 16], ids=["1wave", "2waves", "3waves", "4waves", "8waves", "16waves"])
-def frontier(monkeypatch, request):
+def frontier(plan, request):
     """The frontier kernel with the episodes cut into 1-16 chunk groups (one
     wave of 64 chunks each, chunks of frontier_len(T, groups) ticks; records
     e * 64 G + c, plane padding 256 G + 16 rows per episode)."""
-    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_NW", str(request.param))
+    plan(policy_path="frontier", groups=request.param)
+
+
+def _spilled_waves(roll, n, steps, groups, n_waves):
+    """Waves of the last frontier launch that spilled: the wspill section of the
+    workspace (sgmm_rollout.hip's layout: u64 cmaps | u64 ctr | u32 kinfo |
+    u32 wslots | u32 wspill | planes, 256-byte aligned, records 64 G per episode)."""
+    a256 = lambda x: (x + 255) & ~255
+    nc, nfr = steps // 64 + n + 1, n * 64 * groups
+    off = a256(max(nc, nfr) * 8) + a256(max(nc * 8, nfr * 32)) + a256(nfr * 4) + a256(n * 64 * 4)
+    w = roll._ws[off:off + 4 * n_waves].cpu().numpy().view(np.uint32)
+    return int((w != 0).sum())
 
 
 def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=0.2, phi=0.0005, fee=0.0,
-         n_threads=8, arl=False):
+         n_threads=8, arl=False, roll_out=None):
     from sgmm_amd import synthetic
     lens = np.asarray(lens, np.int64)
     P = len(lens)
@@ -44,8 +54,10 @@ def _run(sgmm, oracle, lens, H, seed, T=None, caps=(2, -2), nan_frac=0.0, sigma=
     params = sgmm.params_tensor([cfg], DEV)
     eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
                            inv_min=i_min, inv_max=i_max).to(DEV)
-    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H,
-                                               adv.to(DEV) if arl else None)
+    roll = sgmm.RolloutEngine(DEV)
+    fit, trd = roll.fitness(ticks, eb, params, pop.to(DEV), H, adv.to(DEV) if arl else None)
+    if roll_out is not None:
+        roll_out.append(roll)
     s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
     want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, adv.numpy() if arl else None,
                                            (s1n, s2n) + tuple(b[2:]), np.arange(P),
@@ -86,12 +98,12 @@ def test_frontier_nan_bounds_fees_wide_population(sgmm, oracle, frontier):
 
 
 @pytest.mark.parametrize("nw", ["", "1", "2", "4"], ids=["default", "1wave", "2waves", "4waves"])
-def test_frontier_default_selection_many_episodes(sgmm, oracle, monkeypatch, nw):
+def test_frontier_default_selection_many_episodes(sgmm, oracle, plan, nw):
     """From 512 episodes on the frontier kernel is the default: 2100 ragged
     episodes bit-exact against the oracle, whole or cut into 2 / 4 chunk
     groups."""
     if nw:
-        monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
+        plan(groups=int(nw))
     lens = 300 + (np.arange(2100) * 37) % 900
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=47, sigma=0.3)
     assert np.array_equal(trd, wt)
@@ -139,6 +151,44 @@ def test_frontier_default_selection_small_shards(sgmm, oracle, n):
     assert np.array_equal(fit, wf)
 
 
+@pytest.mark.parametrize("spill", [1, 20, 28], ids=["spill_all", "spill20", "spill28"])
+@pytest.mark.parametrize("groups,ls", [(1, 1), (2, 1), (4, 2)], ids=["whole", "halves", "quarters_ls2"])
+@pytest.mark.parametrize("H", [16, 32])
+def test_frontier_spill(sgmm, oracle, plan, spill, groups, ls, H):
+    """The spill (k_frontier_spill): walks past the slot budget (spill / 16 slots per
+    tick of the longest walk; 1 = nearly every walk) stop with at most 64 ticks left
+    in their chunks and the rest runs tick-parallel; the path scan reads the
+    completed frontier layout.  Ragged lengths (short last chunks, chunks that had
+    already ended at the stop, 16 / 32 / 64-tick remainders), 5 and 8 states, NaN
+    bounds and fees, whole walks, halves and quarters with two waves per walk --
+    bit-exact against the oracle, with walks actually spilled."""
+    plan(policy_path="frontier", groups=groups, lane_split=ls, spill=spill)
+    lens = [0, 1, 5, 63, 65, 257, 1000, 4097, 4560, 9001, 20000, 4560, 4560, 3600]
+    for caps, nan, fee in (((2, -2), 0.0, 0.0), ((3, -4), 0.03, 3e-5)):
+        rolls = []
+        fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=83, caps=caps, sigma=0.6, nan_frac=nan, fee=fee,
+                                roll_out=rolls)
+        assert np.array_equal(trd, wt)
+        assert np.array_equal(fit, wf)
+        n, steps = len(lens), int(np.sum(lens))
+        nsp = _spilled_waves(rolls[0], n, steps, groups, n * groups * ls)
+        if spill == 1:
+            assert nsp >= n // 2, nsp
+        else:
+            assert nsp >= 0
+
+
+@pytest.mark.parametrize("spill", [1, 24], ids=["spill_all", "spill24"])
+def test_frontier_spill_many_episodes_default_plan(sgmm, oracle, plan, spill):
+    """The spill on the default launch plan of 2 100 ragged H = 32 episodes (the
+    four-walk rule: whole walks and halves): bit-exact against the oracle."""
+    plan(spill=spill)
+    lens = 3000 + (np.arange(2100) * 37) % 1600
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=89, sigma=0.4)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+
+
 def test_frontier_lifts_the_episode_length_cap(sgmm, oracle):
     """Episodes longer than the table's 131072-tick cap run on the frontier
     kernel (agent_trainer.py:74-77 concatenates days without a bound): a
@@ -161,7 +211,7 @@ def test_adversary_episodes_have_no_length_cap(sgmm, oracle, H):
     assert trd[0] > 1000
 
 
-def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
+def test_frontier_training_equals_table(sgmm, tmp_path, plan):
     """DRLEngine (device RNG, fused validation) trains identically with the
     frontier kernel (whole episodes and 3 chunk groups) and the table:
     histories and final masters."""
@@ -171,8 +221,7 @@ def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
     st = synthetic.train_stats(tr)
     out = {}
     for path in ("table", "frontier", "frontier3"):
-        monkeypatch.setenv("SGMM_TABLE_PATH", "frontier" if path.startswith("frontier") else path)
-        monkeypatch.setenv("SGMM_FRONTIER_NW", "3" if path == "frontier3" else "1")
+        plan(policy_path="frontier" if path.startswith("frontier") else path, groups=3 if path == "frontier3" else 1)
         torch.manual_seed(7)
         eng = sgmm.DRLEngine(pop_size=40, phi=0.001, tick_size=0.001, save_dir=str(tmp_path / path), hidden_dim=32,
                              rng="device", seed=99, sync_every=4, verbose=False)
@@ -187,7 +236,7 @@ def test_frontier_training_equals_table(sgmm, tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("val_mode", ["best", "fused"])
-def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mode):
+def test_frontier_multi_population_training(sgmm, tmp_path, plan, val_mode):
     """Three populations (two assets) trained on the frontier kernel (the
     scan's last workgroup per population runs its tell, or its whole GA step
     with fused validation) equal the table path bit for bit
@@ -196,7 +245,7 @@ def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mod
     tr, va, st = R.multi_workload()
     out = {}
     for path in ("table", "frontier"):
-        monkeypatch.setenv("SGMM_TABLE_PATH", path)
+        plan(policy_path=path)
         m = R.multi_engines(sgmm, 30, False, str(tmp_path / path), val_mode, dist=False)
         out[path] = R.multi_result(m, m.train(tr, va, st, generations=8))
     for key in out["table"]:
@@ -204,13 +253,12 @@ def test_frontier_multi_population_training(sgmm, tmp_path, monkeypatch, val_mod
 
 
 @pytest.mark.parametrize("nw", ["1", "2", "4", "8", "16"], ids=["1wave", "2waves", "4waves", "8waves", "16waves"])
-def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
+def test_frontier_one_wave_scan_lengths(sgmm, oracle, plan, nw):
     """Above 512 episodes the path scan is one wave per episode (1024-tick
     windows of a 256-thread layout run by 64 lanes): chunk lengths from 4 to
     past 512 ticks, ragged last windows and chunks, both chunk groups of split
     episodes -- bit-exact against the oracle."""
-    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
+    plan(policy_path="frontier", groups=int(nw))
     base = np.array([17, 255, 4560, 8191, 20001, 30003, 40000, 4097])
     n = 1100
     lens = base[np.arange(n) % len(base)] + (np.arange(n) // len(base)) % 7
@@ -222,13 +270,11 @@ def test_frontier_one_wave_scan_lengths(sgmm, oracle, monkeypatch, nw):
 @pytest.mark.parametrize("ls,nw", [("2", "1"), ("2", "4"), ("4", "1"), ("4", "3")],
                          ids=["2waves_1group", "2waves_4groups", "4waves_1group", "4waves_3groups"])
 @pytest.mark.parametrize("H", [16, 32])
-def test_frontier_lane_split(sgmm, oracle, monkeypatch, ls, nw, H):
+def test_frontier_lane_split(sgmm, oracle, plan, ls, nw, H):
     """Lane split (k_policy_frontier<H, NSI, LS>): two or four waves per 64-chunk
     walk, each walking 32 or 16 of its chunks (the default from S/2 episodes
     down); ragged lengths, every group count, 5 and 8 states -- bit-exact."""
-    monkeypatch.setenv("SGMM_TABLE_PATH", "frontier")
-    monkeypatch.setenv("SGMM_FRONTIER_LS", ls)
-    monkeypatch.setenv("SGMM_FRONTIER_NW", nw)
+    plan(policy_path="frontier", lane_split=int(ls), groups=int(nw))
     lens = [0, 1, 5, 63, 65, 257, 1000, 4097, 4560, 9001]
     for caps in ((2, -2), (3, -4)):
         fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=71, caps=caps, sigma=0.5)

@@ -159,17 +159,10 @@ def test_multi_sharded_ranks_equal_one_process(sgmm, tmp_path, world, P, val_mod
     mp.spawn(R.multi_train_rank, args=(world, port, P, gens, str(tmp_path), val_mode, arl, table_path),
              nprocs=world, join=True)
     tr, va, st = R.multi_workload()
-    old = os.environ.get("SGMM_TABLE_PATH")
-    if table_path:
-        os.environ["SGMM_TABLE_PATH"] = table_path
-    try:
+    from sgmm_amd import _lib
+    with _lib.plan(policy_path=table_path or "auto"):
         single = R.multi_engines(sgmm, P, arl, str(tmp_path / "single"), val_mode, dist=False)
         want = R.multi_result(single, single.train(tr, va, st, generations=gens))
-    finally:
-        if old is None:
-            os.environ.pop("SGMM_TABLE_PATH", None)
-        else:
-            os.environ["SGMM_TABLE_PATH"] = old
     for r in range(world):
         got = np.load(tmp_path / f"m{r}.npz")
         assert sorted(got.files) == sorted(want), r

@@ -286,16 +286,16 @@ def test_scan_ragged_lengths(golden, sgmm, oracle):
 
 
 @pytest.mark.parametrize("path", ["valu", "table", "table_v3", "frontier"])
-def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
+def test_table_paths_agree(golden, sgmm, oracle, path, plan):
     """Every policy kernel -- the VALU table, the f32-MFMA tables (one state per
-    wave for small launches, the v3 schedule forced by SGMM_TABLE_SP=0;
+    wave for small launches, the v3 schedule forced by the table_sp=0 plan override;
     k_policy_table_mfma with the adversary and for H = 64) and the frontier
     kernel -- reproduces the oracle's canonical fma chains bit for bit (the MFMA
     k-order equals the chain)."""
     if path == "table_v3":
-        monkeypatch.setenv("SGMM_TABLE_SP", "0")
+        plan(table_sp=0)
         path = "table"
-    monkeypatch.setenv("SGMM_TABLE_PATH", path)
+    plan(policy_path=path)
     eps = list(episodes_from_fixture(golden("g2_synthetic.npz")))
     eps += _synthetic_batch(sgmm, 4, 1000, 32, seed=77, sigma=0.4)
     for (H, arl), group in _groups(eps).items():
@@ -307,7 +307,7 @@ def test_table_paths_agree(golden, sgmm, oracle, path, monkeypatch):
 
 @pytest.mark.parametrize("caps", [(0, 0), (1, -1), (2, -2), (3, -4)], ids=["nsi1", "nsi3", "nsi5", "nsi8"])
 @pytest.mark.parametrize("H", [16, 32])
-def test_state_parallel_table(sgmm, oracle, caps, H, monkeypatch):
+def test_state_parallel_table(sgmm, oracle, caps, H, plan):
     """The one-state-per-wave table (k_policy_table_sp, launches of at most 256
     chunks) and the v3 table agree bit for bit with each other and the oracle,
     for 1, 3, 5 and 8 inventory states and ragged lengths (partial last chunk,
@@ -326,10 +326,10 @@ def test_state_parallel_table(sgmm, oracle, caps, H, monkeypatch):
     params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0001, tick_size=0.001, i_max=i_max, i_min=i_min)], DEV)
     eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
                            inv_min=i_min, inv_max=i_max).to(DEV)
-    monkeypatch.setenv("SGMM_TABLE_PATH", "table")
+    plan(policy_path="table")
     got = {}
     for sp in ("1", "0"):
-        monkeypatch.setenv("SGMM_TABLE_SP", sp)
+        plan(table_sp=int(sp))
         fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H)
         got[sp] = (fit.cpu().numpy(), trd.cpu().numpy())
     want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, None, (s1n, s2n) + tuple(b[2:]), np.arange(P), None,

@@ -123,12 +123,14 @@ def test_config4_trained_adversaries_match_oracle(sgmm, oracle, tmp_path):
     assert (t > 0).mean() > 0.5
 
 
-def test_config3_walk_reorder_same_results(sgmm, tmp_path, monkeypatch):
+def test_config3_walk_reorder_same_results(sgmm, tmp_path):
     """The walk-order feedback (k_walk_reorder after each training launch of
     sgmm_generation_multi_best: the next launch walks the lightest populations whole)
     only schedules: 8 generations of config 3 with it and without it
-    (SGMM_FRONTIER_REORDER=0) give byte-identical history rows and masters; with it
-    the training batch's order is a permutation of whole population blocks."""
+    (walk_feedback=False: sgmm_populations::walk_order = NULL) give byte-identical
+    history rows and masters; with it the session's walk order is a permutation of
+    whole population blocks, and the episode batch's own order array (the ABI's
+    read-only train_eps->order) is never written."""
     import bench
     spec = dict(bench.CONFIGS[3])
     P, K = spec["P"], len(spec["pops"])
@@ -137,21 +139,23 @@ def test_config3_walk_reorder_same_results(sgmm, tmp_path, monkeypatch):
     va = [data[a][1] for _, _, a in spec["pops"]]
     st = [data[a][2] for _, _, a in spec["pops"]]
     out = {}
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SGMM_FRONTIER_REORDER", flag)
-        d = tmp_path / f"r{flag}"
+    for flag in (True, False):
+        d = tmp_path / f"r{int(flag)}"
         d.mkdir()
-        eng = bench.make_engine(sgmm, spec, P, str(d), None, True, "auto")
+        eng = bench.make_engine(sgmm, spec, P, str(d), None, True, "auto", walk_feedback=flag)
         sess = eng.session(tr, va, st, generations=9)
         sess.steps(0, 8)
         torch.cuda.synchronize()
         out[flag] = (sess.hist[:, :8].cpu().numpy().copy(), sess.masters.cpu().numpy().copy(),
-                     sess.eps.dev["order"].cpu().numpy().copy())
+                     sess.walk_order.cpu().numpy().copy(), sess.eps.dev["order"].cpu().numpy().copy())
         sess.finish()
-    assert np.array_equal(out["1"][0], out["0"][0])
-    assert np.array_equal(out["1"][1], out["0"][1])
-    order = out["1"][2]
+    assert np.array_equal(out[True][0], out[False][0])
+    assert np.array_equal(out[True][1], out[False][1])
+    order = out[True][2]
     assert np.array_equal(np.sort(order), np.arange(K * P))
+    assert not np.array_equal(order, np.arange(K * P)), "the feedback never reordered"
     for b in order.reshape(K, P):
         assert b[0] % P == 0 and np.array_equal(b, b[0] + np.arange(P))
-    assert np.array_equal(out["0"][2], np.arange(K * P))
+    assert np.array_equal(out[False][2], np.arange(K * P))
+    for flag in (True, False):  # the batch's order array is read-only
+        assert np.array_equal(out[flag][3], np.arange(K * P))

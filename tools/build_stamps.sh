@@ -2,4 +2,4 @@
 set -e
 mkdir -p tools/stamps
 python deep-reinforcement-learning-based-signal-gated-market-making_amd/build.py \
-  --out tools/stamps/libsgmm_stamps.so -- -DSGMM_STAMPS "$@"
+  --out tools/stamps/libsgmm_stamps.so -- -DSGMM_STAMPS -DSGMM_EXPERIMENTS "$@"
