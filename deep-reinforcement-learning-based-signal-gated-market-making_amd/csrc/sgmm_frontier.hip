@@ -68,7 +68,9 @@ __device__ unsigned int g_thwid[kStampWaves][2];  // HW_ID, XCC_ID of each wave
 // 64 / LS of the group's chunks (lanes past them idle): the same chunks, the
 // same chunk starts, LS times the waves -- for launches with fewer walks than
 // the SIMDs hold.
-template <int H, int NSI, int LS>
+// SP: the spill variant (FrontierArgs::wspill / spill_budget); without it the
+// walk loop compiles exactly as before (its registers sit at the 128-VGPR edge)
+template <int H, int NSI, int LS, bool SP>
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void k_policy_frontier(FrontierArgs args) {
     static_assert(H % 16 == 0 && H <= 32, "frontier kernel: H = 16 or 32");
     using L = GenomeLayout<H>;
@@ -90,10 +92,12 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     __shared__ uint32_t nslot_s;  // MLP slots run (FrontierArgs::wslots; in LDS: the walk loop has no register to spare)
     // spill bookkeeping in LDS (no register is spare in the walk loop): this wave's
     // id, the first tick offset it may stop at, its slot budget
-    __shared__ uint32_t wid_s, tmin_s, sbud_s;
-    if (threadIdx.x == 0) {  // every wave of the launch writes its spill entry, spilled or not
+    __shared__ uint32_t wid_s, tmin_s, t0_s, spk_s;
+    if (SP && threadIdx.x == 0) {  // every wave of the launch writes its spill entry, spilled or not
         wid_s = blockIdx.x;
-        if (args.wspill) args.wspill[blockIdx.x] = 0u;
+        spk_s = 0;
+        t0_s = (uint32_t)wall_clock64();  // 100 MHz
+        args.wspill[blockIdx.x] = 0u;
     }
 
     const sgmm_ticks& tk = args.tk;
@@ -112,14 +116,10 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     const int off = ((int)blockIdx.x % LS) * NL;  // this wave's first chunk within the group
     const int e = ep.order ? ep.order[pos] : pos;
     const int32_t T = ep.len[e];
-    const int CL = frontier_len(max(T, 1), nw);
+    if (T <= 0) return;  // block-uniform
+    const int CL = frontier_len(T, nw);
     const int nch = (T + CL - 1) / CL;
-    if (T <= 0 || cg * kFrontierLanes + off >= nch) {  // block-uniform: no chunk here
-        // (a walk with no chunk still has a slot count for the walk-order feedback: 0)
-        if (LS == 1 && threadIdx.x == 0 && args.wslots)
-            args.wslots[frontier_rec(e, ep.ngrp, cg * kFrontierLanes + off) / NL] = 0u;
-        return;
-    }
+    if (cg * kFrontierLanes + off >= nch) return;  // a group (part) past the episode's last chunk
     const int lane = (int)threadIdx.x, grp = lane >> 4, col = lane & 15;
     const bool lane_ok = LS == 1 || lane < NL;
     const int c = cg * kFrontierLanes + off + lane;    // this lane's chunk
@@ -195,10 +195,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
     int64_t ti = tick_of(0);
     float ns1 = tk.s1n[ti], ns2 = tk.s2n[ti];  // the signals one tick ahead
     int fr_extra = 0;
-    if (lane == 0) {
+    if ((SP || LS == 1) && lane == 0) {
         nslot_s = 0;
-        sbud_s = args.spill_budget;
-        tmin_s = args.spill_budget ? (uint32_t)max(4, CL - kSpillTicks) : 0xFFFFFFFFu;
+        if (SP) tmin_s = (uint32_t)max(4, CL - kSpillTicks);
     }
 
     // layers 1-3 for the columns of this slot (their inputs in the rows of
@@ -289,18 +288,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
 #ifdef SGMM_STAMPS_PHASE
         SGMM_FT(fs_b);
 #endif
-        // spill: a walk past the launch's slot budget stops here once its chunks
-        // have at most kSpillTicks ticks left; k_frontier_spill finishes them
-        // tick-parallel from the records written below (every 4 ticks)
-        if ((tt & 3) == 0 && (uint32_t)tt >= (uint32_t)__builtin_amdgcn_readfirstlane((int)tmin_s)) {
-            const uint32_t ns = (uint32_t)__builtin_amdgcn_readfirstlane(
-                (int)__hip_atomic_load(&nslot_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
-            if (ns > (uint32_t)__builtin_amdgcn_readfirstlane((int)sbud_s)) {
-                if (lane == 0) {
-                    args.wspill[wid_s] = (uint32_t)tt;
-                    // the walk-order feedback's count: extrapolated to the whole walk
-                    nslot_s = (uint32_t)((uint64_t)ns * (uint32_t)CL / (uint32_t)tt);
-                }
+        // spill: a walk still running at the launch's deadline (spill_budget, in
+        // 10 ns since the wave started) stops here once its chunks have at most
+        // kSpillTicks ticks left; k_frontier_spill finishes them tick-parallel from
+        // the records written below (checked every 4 ticks)
+        if constexpr (SP) {
+            if ((tt & 3) == 0 && (uint32_t)tt >= (uint32_t)__builtin_amdgcn_readfirstlane((int)tmin_s) &&
+                (uint32_t)wall_clock64() - (uint32_t)__builtin_amdgcn_readfirstlane((int)t0_s) > args.spill_budget) {
+                if (lane == 0) spk_s = (uint32_t)tt;
                 break;
             }
         }
@@ -346,7 +341,7 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         // apart: a heavy walk, the launch's tail) takes the SIMD's issue
         // priority over the light walks beside it (round 4, profiles/r04_ab)
         fr_extra = fr_extra - (fr_extra >> 3) + (nx << 5);  // decaying average of extra slots per tick, x 256
-        if (lane == 0)
+        if ((SP || LS == 1) && lane == 0)
             __hip_atomic_fetch_add(&nslot_s, (uint32_t)((any0 ? 1 : 0) + nx), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
         if ((tt & 7) == 7) {
             if (fr_extra > kFrPrioExtra) __builtin_amdgcn_s_setprio(2);
@@ -534,6 +529,14 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(4))) void
         }
     }
 #endif
+    if (SP && lane == 0) {
+        const uint32_t k = spk_s;
+        if (k) {  // spilled: the entry for k_frontier_spill, and the walk-order feedback's
+                  // slot count extrapolated to the whole walk
+            args.wspill[wid_s] = k;
+            nslot_s = __hip_atomic_load(&nslot_s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) * (uint32_t)CL / k;
+        }
+    }
     if (lane_ok && c < nch) {
         // untracked start states keep the identity byte (never on the episode's path)
         uint64_t cm = kIdentityMap;
@@ -816,11 +819,16 @@ int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStr
     const dim3 grid(n_waves), block(kWave);
     {
         const dim3 gs(n_waves * (unsigned)ls);
-#define SGMM_FR_LAUNCH(H_, N_)                                                                   \
+#define SGMM_FR_LAUNCH2(H_, N_, SP_)                                                             \
     do {                                                                                         \
-        if (ls == 4) SGMM_LAUNCH((k_policy_frontier<H_, N_, 4>), gs, block, 0, s, fa);           \
-        else if (ls == 2) SGMM_LAUNCH((k_policy_frontier<H_, N_, 2>), gs, block, 0, s, fa);      \
-        else SGMM_LAUNCH((k_policy_frontier<H_, N_, 1>), grid, block, 0, s, fa);                 \
+        if (ls == 4) SGMM_LAUNCH((k_policy_frontier<H_, N_, 4, SP_>), gs, block, 0, s, fa);      \
+        else if (ls == 2) SGMM_LAUNCH((k_policy_frontier<H_, N_, 2, SP_>), gs, block, 0, s, fa); \
+        else SGMM_LAUNCH((k_policy_frontier<H_, N_, 1, SP_>), grid, block, 0, s, fa);            \
+    } while (0)
+#define SGMM_FR_LAUNCH(H_, N_)                                \
+    do {                                                      \
+        if (fa.spill_budget && fa.wspill) SGMM_FR_LAUNCH2(H_, N_, true); \
+        else SGMM_FR_LAUNCH2(H_, N_, false);                  \
     } while (0)
         if (hidden == 16) {
             if (nsi <= 5) SGMM_FR_LAUNCH(16, 5);
@@ -830,6 +838,7 @@ int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStr
             else SGMM_FR_LAUNCH(32, 8);
         }
 #undef SGMM_FR_LAUNCH
+#undef SGMM_FR_LAUNCH2
     }
     SGMM_LAUNCHED();
     return SGMM_OK;

@@ -225,7 +225,7 @@ struct FrontierArgs {
     uint32_t* wslots;  // one wave per walk: [e * ngrp + cg] = the MLP slots it ran (walk-order feedback), or null
     // spill (k_frontier_spill): wave b of the launch writes wspill[b] = the tick
     // offset at which it stopped (a multiple of 4, > 0), or 0 when it walked to
-    // the end; a walk stops once its MLP slots pass spill_budget (0: never) and
+    // the end; a walk stops once it has run spill_budget x 10 ns (0: never) and
     // its chunks have at most kSpillTicks ticks left
     uint32_t* wspill;
     uint32_t spill_budget;

@@ -2121,8 +2121,14 @@ static FrontierPlan frontier_plan(int32_t n) {
     // SGMM_PLAN_TAIL = 0 keeps every walk whole.
     const bool tail = plan_value(SGMM_PLAN_TAIL) != 0;
     const int64_t r = n % S;
-    const bool four = plan_value(SGMM_PLAN_FOUR) != 0;  // experiments: 0 = no four-walk rule
-    if (tail && four && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
+    const int fourv = plan_value(SGMM_PLAN_FOUR);
+    const bool four = fourv != 0;  // experiments: 0 = no four-walk rule, 2 = whole walks and quarters
+    if (tail && fourv == 2 && p.g0 == 1 && 4 * n - 4 * S >= 3 * (S / 2) && n < 4 * S) {
+        // experiment: four walks per SIMD as whole walks and quarters, (4n - 4S) / 3
+        // whole (config 3: 2048 whole + 512 episodes in quarters)
+        p.whole = (int32_t)((4 * n - 4 * S) / 3);
+        p.gtail = p.gmax = 4;
+    } else if (tail && four && p.g0 == 1 && 2 * n - 4 * S >= S / 2 && n < 4 * S) {
         // from 2.5 episodes per SIMD up to 4: four walks per SIMD, 2n - 4S whole
         // and the rest in halves, one whole and three half walks per SIMD (config
         // 3: 2560 = 1024 whole + 1536 in halves; 660.5-668.0 against 670.3-670.6 us
@@ -2143,17 +2149,16 @@ static FrontierPlan frontier_plan(int32_t n) {
 // the record / plane-padding layout of a launch of n episodes
 static int32_t frontier_groups(int32_t n) { return frontier_plan(n).gmax; }
 
-// Spill budget of a frontier launch in MLP slots per walk: SGMM_PLAN_SPILL / 16
-// slots per tick of the launch's longest walk (its g0-group chunks), 0 = no
-// spill.  A walk stops once past it and its chunks have <= kSpillTicks ticks
-// left; k_frontier_spill runs the rest tick-parallel.
+// Spill deadline of a frontier launch (FrontierArgs::spill_budget, 10 ns units):
+// SGMM_PLAN_SPILL microseconds after a walk's start, 0 = no spill.  A walk
+// still running then stops once its chunks have <= kSpillTicks ticks left;
+// k_frontier_spill runs the rest tick-parallel.
 constexpr int kSpillDefault = 0;
-static uint32_t spill_budget(const sgmm_episodes* eps, const FrontierPlan& plan) {
+static uint32_t spill_budget(const sgmm_episodes* eps, const FrontierPlan&) {
     int v = plan_value(SGMM_PLAN_SPILL);
     if (v < 0) v = kSpillDefault;
     if (v == 0 || eps->max_len <= 0) return 0;
-    const int64_t cl = frontier_len(eps->max_len, plan.g0);
-    return (uint32_t)std::max<int64_t>(1, (int64_t)v * cl / 16);
+    return (uint32_t)std::min<int64_t>((int64_t)v * 100, 0x7FFFFFFF);
 }
 
 
@@ -2394,7 +2399,7 @@ static bool walk_reorder(const sgmm_episodes* eps, const FrontierPlan& plan, con
     const int P = src.pop_eps;
     return walk_order && eps->order == walk_order && P > 0 && eps->n % P == 0 && eps->n / P >= 2 &&
            eps->n / P <= kReorderMaxPops &&
-           plan.ls == 1 && plan.g0 == 1 && plan.gtail == 2 && plan.whole > 0 && plan.whole < eps->n &&
+           plan.ls == 1 && plan.g0 == 1 && (plan.gtail == 2 || plan.gtail == 4) && plan.whole > 0 && plan.whole < eps->n &&
            eps->total_steps == (int64_t)eps->n * eps->max_len;
 }
 

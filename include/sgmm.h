@@ -492,7 +492,7 @@ enum {
     SGMM_PLAN_TABLE_SP = 6,      /* 0 / 1: state-parallel table off / forced */
     SGMM_PLAN_SCAN_THREADS = 7,  /* path-scan workgroup: 64, 256, 512 or 1024 */
     SGMM_PLAN_REORDER_WEIGHTS = 8, /* walk-order scores: whole << 8 | split */
-    SGMM_PLAN_SPILL = 9,         /* frontier spill budget, MLP slots per walk tick x 16 (0: off) */
+    SGMM_PLAN_SPILL = 9,         /* frontier spill deadline, us after a walk's start (0: off) */
     SGMM_PLAN_N = 10
 };
 int sgmm_plan_set(int32_t knob, int32_t value);

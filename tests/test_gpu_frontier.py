@@ -151,13 +151,13 @@ def test_frontier_default_selection_small_shards(sgmm, oracle, n):
     assert np.array_equal(fit, wf)
 
 
-@pytest.mark.parametrize("spill", [1, 20, 28], ids=["spill_all", "spill20", "spill28"])
+@pytest.mark.parametrize("spill", [1, 60, 150], ids=["spill_all", "spill60us", "spill150us"])
 @pytest.mark.parametrize("groups,ls", [(1, 1), (2, 1), (4, 2)], ids=["whole", "halves", "quarters_ls2"])
 @pytest.mark.parametrize("H", [16, 32])
 def test_frontier_spill(sgmm, oracle, plan, spill, groups, ls, H):
-    """The spill (k_frontier_spill): walks past the slot budget (spill / 16 slots per
-    tick of the longest walk; 1 = nearly every walk) stop with at most 64 ticks left
-    in their chunks and the rest runs tick-parallel; the path scan reads the
+    """The spill (k_frontier_spill): walks still running `spill` us after their start
+    (1 = every walk, at its first allowed tick) stop with at most 64 ticks left in
+    their chunks and the rest runs tick-parallel; the path scan reads the
     completed frontier layout.  Ragged lengths (short last chunks, chunks that had
     already ended at the stop, 16 / 32 / 64-tick remainders), 5 and 8 states, NaN
     bounds and fees, whole walks, halves and quarters with two waves per walk --
@@ -178,7 +178,7 @@ def test_frontier_spill(sgmm, oracle, plan, spill, groups, ls, H):
             assert nsp >= 0
 
 
-@pytest.mark.parametrize("spill", [1, 24], ids=["spill_all", "spill24"])
+@pytest.mark.parametrize("spill", [1, 100], ids=["spill_all", "spill100us"])
 def test_frontier_spill_many_episodes_default_plan(sgmm, oracle, plan, spill):
     """The spill on the default launch plan of 2 100 ragged H = 32 episodes (the
     four-walk rule: whole walks and halves): bit-exact against the oracle."""

@@ -22,7 +22,13 @@ is trained on the device for 24 generations, and then:
      the pinned one.
 
 The same for BASELINE config 4's shape (256 market makers + 256 adversaries,
-paired i <-> i, drl_engine.py:104-115) with trained adversaries.
+paired i <-> i, drl_engine.py:104-115) with trained adversaries, and for BASELINE
+config 5 (two assets x 4096, tick sizes 0.001 and 0.01) whole and as the per-rank
+shards of its 8- and 16-GPU runs (`bench.py --shard-of 8 / 16`: 2 x 512 episodes
+in two chunk groups, 2 x 256 in four groups with two waves per walk) -- the launch
+plans the strong-scaled runs take, on the populations they would train.  The
+frontier spill (k_frontier_spill) is pinned the same way on config 3's trained
+state, every walk forced to spill.
 """
 import os
 
@@ -39,7 +45,7 @@ DEV = torch.device("cuda:0")
 THREADS = max(1, min(16, os.cpu_count() or 1))
 
 
-def _pin_trained(sgmm, oracle, tmp_path, config, gens):
+def _pin_trained(sgmm, oracle, tmp_path, config, gens, shard_of=1, plan=None):
     import bench
     from sgmm_amd import _lib
     from sgmm_amd.drl_engine import ADV_GENOME, HIST_DTYPE
@@ -47,6 +53,9 @@ def _pin_trained(sgmm, oracle, tmp_path, config, gens):
 
     spec = dict(bench.CONFIGS[config])
     P, H, T = spec["P"], spec["H"], spec["T"]
+    if shard_of > 1:  # one rank's shard of the strong-scaled run (bench.py --shard-of)
+        from sgmm_amd.shard import shard_capacity
+        P = shard_capacity(P, shard_of)
     K = len(spec["pops"])
     G = genome_size(H)
     data = bench.bundles(spec)
@@ -82,8 +91,19 @@ def _pin_trained(sgmm, oracle, tmp_path, config, gens):
     ep_adv = np.arange(K * P) if adv is not None else None
     eps = sgmm.EpisodeBatch(np.arange(K * P), offs, lens, par, adv=ep_adv).to(DEV)
     params = sgmm.params_tensor([sgmm.EnvConfig(phi=phi, tick_size=tick) for phi, tick, _ in spec["pops"]], DEV)
-    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eps, params, pop, H, adv)
+    with _lib.plan(**(plan or {})):
+        _lib.profile_read()
+        _lib.profile_enable(True)
+        try:
+            fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eps, params, pop, H, adv)
+            kernels = _lib.profile_read()
+        finally:
+            _lib.profile_enable(False)
     torch.cuda.synchronize()
+    if not spec["arl"]:
+        assert "policy_frontier" in kernels, kernels  # the launch plan under test
+    if plan and plan.get("spill"):
+        assert "frontier_spill" in kernels, kernels
     got_f, got_t = fit.cpu().numpy(), trd.cpu().numpy()
 
     cols = [[], [], [], [], [], [], []]
@@ -123,6 +143,23 @@ def test_config4_trained_adversaries_match_oracle(sgmm, oracle, tmp_path):
     assert (t > 0).mean() > 0.5
 
 
+@pytest.mark.parametrize("shard_of", [1, 8, 16], ids=["whole", "shard_1_of_8", "shard_1_of_16"])
+def test_config5_trained_populations_match_oracle(sgmm, oracle, tmp_path, shard_of):
+    """Config 5 (2 x 4096, two assets) trained 20 generations on one GPU, and the
+    per-rank shards of its 8- and 16-GPU runs trained as `bench.py --shard-of`
+    trains them (2 x 512 episodes: two chunk groups per episode; 2 x 256: four
+    groups, two waves per walk): bit-exact against the oracle."""
+    f, t = _pin_trained(sgmm, oracle, tmp_path, config=5, gens=20, shard_of=shard_of)
+    assert (t > 0).mean() > 0.5
+
+
+def test_config3_trained_spill_match_oracle(sgmm, oracle, tmp_path):
+    """The frontier spill on the benchmarked state: config 3 trained 24
+    generations, every walk stopped at its first allowed tick (a 1 us deadline)
+    and finished tick-parallel by k_frontier_spill -- bit-exact."""
+    _pin_trained(sgmm, oracle, tmp_path, config=3, gens=24, plan={"spill": 1})
+
+
 def test_config3_walk_reorder_same_results(sgmm, tmp_path):
     """The walk-order feedback (k_walk_reorder after each training launch of
     sgmm_generation_multi_best: the next launch walks the lightest populations whole)
@@ -153,9 +190,21 @@ def test_config3_walk_reorder_same_results(sgmm, tmp_path):
     assert np.array_equal(out[True][1], out[False][1])
     order = out[True][2]
     assert np.array_equal(np.sort(order), np.arange(K * P))
-    assert not np.array_equal(order, np.arange(K * P)), "the feedback never reordered"
     for b in order.reshape(K, P):
         assert b[0] % P == 0 and np.array_equal(b, b[0] + np.arange(P))
     assert np.array_equal(out[False][2], np.arange(K * P))
     for flag in (True, False):  # the batch's order array is read-only
         assert np.array_equal(out[flag][3], np.arange(K * P))
+    # the feedback does rewrite the walk order (eager generations, read after each;
+    # which population is heaviest moves with training, so any one read may be the identity)
+    d = tmp_path / "eager"
+    d.mkdir()
+    eng = bench.make_engine(sgmm, spec, P, str(d), None, False, "auto")
+    sess = eng.session(tr, va, st, generations=4)
+    seen = []
+    for g in range(3):
+        sess.step(g)
+        torch.cuda.synchronize()
+        seen.append(sess.walk_order.cpu().numpy().copy())
+    sess.finish()
+    assert any(not np.array_equal(o, np.arange(K * P)) for o in seen), "the feedback never reordered"
