@@ -726,13 +726,18 @@ struct ReorderJob {
     const uint32_t* wslots;
     int32_t* order;  // null: no job
     int32_t n, whole, gtail, pop_eps;
-    uint32_t w_whole = 5, w_split = 4;  // score weights (SGMM_REORDER_WEIGHTS=whole,split for experiments)
+    uint32_t w_whole = 5, w_split = 4;  // score weights (SGMM_PLAN_REORDER_WEIGHTS for experiments)
+    int32_t len = 0;                    // the episodes' (common) length: groups past the last chunk have no count
 };
 __device__ __forceinline__ void walk_reorder_block(const ReorderJob rj) {
     const uint32_t* __restrict__ wslots = rj.wslots;
     int32_t* __restrict__ order = rj.order;
     const int32_t n = rj.n, whole = rj.whole, gtail = rj.gtail, pop_eps = rj.pop_eps;
     const int nt = (int)blockDim.x;
+    // an episode in gtail groups has chunks in the first ceil(nch / 64) only (the
+    // frontier kernel writes no slot count for an empty group)
+    const int cl = frontier_len(max(rj.len, 1), gtail);
+    const int gused = min(gtail, (((rj.len + cl - 1) / cl) + kFrontierLanes - 1) / kFrontierLanes);
     __shared__ uint32_t score[kReorderMaxPops];
     __shared__ int32_t rank[kReorderMaxPops];
     const int npop = n / pop_eps;
@@ -758,7 +763,7 @@ __device__ __forceinline__ void walk_reorder_block(const ReorderJob rj) {
                 sc[j] = rj.w_whole * wslots[e[j] * gtail];
             } else {
                 uint32_t sum = 0;
-                for (int g = 0; g < gtail; ++g) sum += wslots[e[j] * gtail + g];
+                for (int g = 0; g < gused; ++g) sum += wslots[e[j] * gtail + g];
                 sc[j] = rj.w_split * sum;
             }
         }
@@ -965,7 +970,7 @@ constexpr int kSumTpt = 4;          // rewards gathered per path-scan thread
 constexpr int kScanThreads = 1024;  // path-scan workgroup
 constexpr int kScanWin = kScanThreads * kSumTpt;
 constexpr int kScanAt1024 = 256;  // path-scan workgroup: 1024 threads up to this many episodes,
-constexpr int kScanAt512 = 512;   // 512 up to this many, one wave above
+constexpr int kScanAt512 = 512;   // 256 up to this many, one wave above
 constexpr int kScanArlAt1024 = 1024;  // adversary path scan: 1024 threads up to this many, kScanBlock above
 constexpr int64_t kMLo = (1LL << 52) + 1, kMHi = (1LL << 53) - 1;
 constexpr int32_t kZeroRun = INT32_MAX;  // a block's prediction: all its values are +-0.0
@@ -2368,8 +2373,11 @@ static int scan_threads(int64_t n) {
     // beyond 512 episodes one-wave workgroups: the exact-sum walk is serial,
     // so many episodes resident per CU beat fewer wider workgroups (config 3:
     // 193 -> 145 us per scan, tools/gpu_sc1.sh; config 5's 1-of-8 shard, 1024
-    // episodes: 110 -> 74 us, profiles/r04_ab/r04k_*)
-    return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 512 : kWave);
+    // episodes: 110 -> 74 us, profiles/r04_ab/r04k_*; round 6: 54.7 against 69.3 /
+    // 94.6 us for 256 / 512 threads, profiles/r06_scanw/).  From 257 to 512
+    // episodes 4-wave workgroups (1024-tick windows): config 5's 1-of-16 shard
+    // (512 episodes) 49.8 against 61.7 us with 512 threads, 52.4 with one wave
+    return n <= kScanAt1024 ? kScanThreads : (n <= kScanAt512 ? 256 : kWave);
 }
 
 template <int NSM, bool FR>
@@ -2551,6 +2559,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     SGMM_LAUNCHED();
     if (fr && step.st && step.mode == 3 && walk_reorder(eps, plan, src, walk_order)) {
         ReorderJob job{wslots, walk_order, eps->n, plan.whole, plan.gtail, src.pop_eps};
+        job.len = eps->max_len;  // equal-length episodes (walk_reorder)
         if (const int w = plan_value(SGMM_PLAN_REORDER_WEIGHTS); w > 0 && (w >> 8) > 0 && (w & 255) > 0) {
             job.w_whole = (uint32_t)(w >> 8) & 63u;
             job.w_split = (uint32_t)w & 63u;

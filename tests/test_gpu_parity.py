@@ -205,17 +205,21 @@ def test_bench_config_population(sgmm, oracle):
     assert np.array_equal(fit, want_f)
 
 
-@pytest.mark.parametrize("n_ep,caps,H", [(n, c, 16) for n in (400, 600, 1100) for c in ((2, -2), (3, -4))] +
-                         [(n, (2, -2), h) for n in (600, 1100) for h in (8, 64)])
-def test_many_episode_scan(sgmm, oracle, n_ep, caps, H):
-    """More than 256 / 512 episodes take the 8-wave / one-wave path scan (2048- /
-    1024-tick windows; at H=16 400 episodes run the table, 600 and 1100 the
+@pytest.mark.parametrize("n_ep,caps,H,width", [(n, c, 16, None) for n in (400, 600, 1100) for c in ((2, -2), (3, -4))] +
+                         [(n, (2, -2), h, None) for n in (600, 1100) for h in (8, 64)] +
+                         [(400, (2, -2), 16, w) for w in (64, 512, 1024)] + [(1100, (3, -4), 16, 256)])
+def test_many_episode_scan(sgmm, oracle, plan, n_ep, caps, H, width):
+    """More than 256 / 512 episodes take the 4-wave / one-wave path scan (1024-tick
+    windows; every width forced by the scan_threads plan override as well: 64,
+    256, 512, 1024 threads; at H=16 400 episodes run the table, 600 and 1100 the
     frontier kernel; H=8 and H=64 have no frontier kernel, so 600 and 1100
     episodes take the table path into the one-wave scan): ragged lengths around
     their window boundaries, every episode bit-exact; with 5 inventory states
     (the default caps) and with 8 (i_max=3, i_min=-4: the NSM=8 scan
     instantiations)."""
     i_max, i_min = caps
+    if width:
+        plan(scan_threads=width)
     from sgmm_amd import synthetic
     T = 5000
     base = [0, 1, 17, 1023, 1024, 1025, 2047, 2048, 2049, 3600, 4096, 5000]

@@ -160,16 +160,20 @@ def test_config3_trained_spill_match_oracle(sgmm, oracle, tmp_path):
     _pin_trained(sgmm, oracle, tmp_path, config=3, gens=24, plan={"spill": 1})
 
 
-def test_config3_walk_reorder_same_results(sgmm, tmp_path):
+@pytest.mark.parametrize("T", [4560, 200], ids=["config3", "short_episodes"])
+def test_config3_walk_reorder_same_results(sgmm, tmp_path, T):
     """The walk-order feedback (k_walk_reorder after each training launch of
     sgmm_generation_multi_best: the next launch walks the lightest populations whole)
     only schedules: 8 generations of config 3 with it and without it
     (walk_feedback=False: sgmm_populations::walk_order = NULL) give byte-identical
     history rows and masters; with it the session's walk order is a permutation of
     whole population blocks, and the episode batch's own order array (the ABI's
-    read-only train_eps->order) is never written."""
+    read-only train_eps->order) is never written.  With 200-tick episodes the
+    halves' second chunk group is empty (no slot count): the feedback scores only
+    the groups that have chunks."""
     import bench
     spec = dict(bench.CONFIGS[3])
+    spec["T"] = T
     P, K = spec["P"], len(spec["pops"])
     data = bench.bundles(spec)
     tr = [data[a][0] for _, _, a in spec["pops"]]
@@ -195,6 +199,8 @@ def test_config3_walk_reorder_same_results(sgmm, tmp_path):
     assert np.array_equal(out[False][2], np.arange(K * P))
     for flag in (True, False):  # the batch's order array is read-only
         assert np.array_equal(out[flag][3], np.arange(K * P))
+    if T != 4560:
+        return
     # the feedback does rewrite the walk order (eager generations, read after each;
     # which population is heaviest moves with training, so any one read may be the identity)
     d = tmp_path / "eager"
