@@ -57,6 +57,10 @@ seg = ticks.segments[ticks.add(tr[0], st[0])]
 ticks.to(DEV)
 n = K * P
 eps = sg.EpisodeBatch(np.arange(n), np.full(n, seg[0]), np.full(n, T), np.repeat(np.arange(K), P))
+if os.environ.get("N_EPS"):  # N_EPS=64: 64 lone walks of population 0 (each alone on its SIMD; PHASE stamps rows = episodes)
+    n = int(os.environ["N_EPS"])
+    eps = sg.EpisodeBatch(np.arange(n), np.full(n, seg[0]), np.full(n, T), np.zeros(n))
+    _lib.plan_set(policy_path="frontier", groups=1, min_eps=1)
 if os.environ.get("ORDER"):  # population order of the walks (the first ones are whole walks), e.g. ORDER=1,4,0,2,3
     eps.order = np.concatenate([np.arange(k * P, (k + 1) * P) for k in map(int, os.environ["ORDER"].split(","))]
                                ).astype(np.int32)
