@@ -30,6 +30,9 @@ struct EpArrays {
     // path scan reads an episode's group count from its first record
     int32_t ngrp;
     int32_t g0, gtail, whole;
+    // path scans: the episode sums as the plain sequential chain (1) or by the
+    // exact parallel binade method (0) -- the same bits either way (rollout_impl's rule)
+    int32_t seq_sum = 0;
 };
 
 // Where an episode's genomes come from: materialized rows (pop != nullptr) or

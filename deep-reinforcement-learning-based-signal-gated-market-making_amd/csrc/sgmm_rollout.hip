@@ -1050,8 +1050,47 @@ struct SumLds {
 // A block without a prediction takes the rest of its run with it: one loop of
 // reference additions, no walk step per block (see the walk below).
 template <int NT>
-__device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L) {
+__device__ __forceinline__ double exact_sum_window(const double* sel, int n, double S, SumLds<NT>& L,
+                                                   bool seq = false) {
     static_assert(NT % (4 * kWave) == 0, "whole block waves");
+    if (seq) {
+        // the plain sequential chain: wave 0's lanes add the window from LDS
+        // broadcast reads in the reference's order, one dependent add per value
+        // (32 values per LDS round trip: 71 against 75 us with 16 on config 3, 64
+        // need 226 VGPRs -- two waves per SIMD).  Faster than the parallel method below
+        // where its fallbacks are many or its window phases are not hidden (the
+        // one-wave scans of thousands of GA-trained episodes, the validation
+        // scans); rollout_impl chooses (scan_seq_sum)
+        if (threadIdx.x < kWave) {
+            double s = S;
+            const double2* p = reinterpret_cast<const double2*>(sel);
+            const int n16 = n & ~15;
+            int i = 0;
+            // (pinning the next 16 values ahead of this 16's adds -- asm operands, which
+            // wait for them -- measured slower: 99 against 76 us on config 3,
+            // profiles/r06_seq2_*)
+#ifndef SGMM_SEQ_CHUNK
+#define SGMM_SEQ_CHUNK 32
+#endif
+            constexpr int kC = SGMM_SEQ_CHUNK;
+            const int nc = n & ~(kC - 1);
+            for (; i < nc; i += kC) {
+                double2 v[kC / 2];
+#pragma unroll
+                for (int j = 0; j < kC / 2; ++j) v[j] = p[i / 2 + j];
+#pragma unroll
+                for (int j = 0; j < kC / 2; ++j) {
+                    s += v[j].x;
+                    s += v[j].y;
+                }
+            }
+            (void)n16;
+            for (; i < n; ++i) s += sel[i];
+            if (threadIdx.x == 0) L.S = s;
+        }
+        __syncthreads();
+        return L.S;
+    }
     constexpr int NB = NT / 4;         // 16-value blocks per window
     constexpr int NWB = NB / kWave;    // waves holding one block per lane
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid >> 6;
@@ -1642,7 +1681,7 @@ __device__ __forceinline__ void scan_episode(int e, int nw, const EpArrays& ep, 
         sw_g += sw_b - sw_a;
 #endif
         if (w0 + kWin < T) gather(w0 + kWin);  // in flight during the sum
-        S = exact_sum_window<NT>(sel, n, S, *sh.L);
+        S = exact_sum_window<NT>(sel, n, S, *sh.L, ep.seq_sum != 0);
 #ifdef SGMM_STAMPS
         SGMM_SW(sw_a);
         sw_s += sw_a - sw_b;
@@ -1854,7 +1893,7 @@ __global__ __launch_bounds__(NT) void k_path_scan_arl(
         __syncthreads();
         SGMM_STAMP(e, 12);
         for (int k = 0; k < segn; k += 4 * NT)  // windows of 4 values per thread
-            total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L);
+            total = exact_sum_window<NT>(sel + k, min(4 * NT, segn - k), total, L, ep.seq_sum != 0);
     }
     int w = my_trades;
 #pragma unroll
@@ -2399,6 +2438,22 @@ static void launch_path_scan(int nt, int64_t n, size_t lds, hipStream_t s, const
                     rew, fitness, trades, step);
 }
 
+// Episode sums of a path scan: the plain sequential chain or the exact parallel
+// binade method (exact_sum_window); both give the reference's bits.  Measured per
+// shape, 20 generations each (profiles/r06_seq/): the sequential chain wins in the
+// one-wave and 4-wave scans of many GA-trained episodes -- config 3 89.0 -> 75.7 us,
+// config 5's 8 192 / 4 096 / 2 048 / 1 024 / 512 episodes 187.9 / 112.8 / 68.0 /
+// 55.9 / 50.7 -> 177.4 / 102.4 / 61.8 / 40.1 / 32.9 us -- and in the validation
+// scans (11.5-12.7 -> 10.3-11.4 us); the parallel method wins where one 16-wave
+// workgroup sums each long episode (config 2 15.7 vs 26.8 us, config 6 18.5 vs
+// 27.0) and in the adversary scan (config 4 39.9 vs 44.9, its 1-of-4 shard 32.5 vs
+// 41.9).  SGMM_PLAN_SEQ_SUM forces either.
+static bool scan_seq_sum(int nt, bool arl, bool validation) {
+    if (const int v = plan_value(SGMM_PLAN_SEQ_SUM); v >= 0) return v != 0;
+    if (validation) return true;
+    return !arl && nt <= 256;
+}
+
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
 // per walk, whole populations of equal-length episodes, the caller's writable
 // walk order (sgmm_populations::walk_order)
@@ -2523,6 +2578,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         // 16-wave workgroups while one per CU fits (a 4096-tick segment is one
         // exact-sum window), 4-wave ones beyond
         const int nt = eps->n <= kScanArlAt1024 ? kScanThreads : kScanBlock;
+        ep.seq_sum = scan_seq_sum(nt, true, vt) ? 1 : 0;
         size_t lds = arl_scan_lds(ns);
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
         if (nt == kScanThreads)
@@ -2538,6 +2594,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         // resident per CU, so the serial walks of different episodes overlap
         // instead of idling the CU (A/B on MI355X: P=64 / 256 / 1024 / 4096)
         const int nt = scan_threads(eps->n);
+        ep.seq_sum = scan_seq_sum(nt, false, vt) ? 1 : 0;
         size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double);  // the window
         if (fr) lds += (size_t)5 * kFrontierLanes * ep.ngrp;  // chunk start states + merge info
         if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));

@@ -493,7 +493,8 @@ enum {
     SGMM_PLAN_SCAN_THREADS = 7,  /* path-scan workgroup: 64, 256, 512 or 1024 */
     SGMM_PLAN_REORDER_WEIGHTS = 8, /* walk-order scores: whole << 8 | split */
     SGMM_PLAN_SPILL = 9,         /* frontier spill deadline, us after a walk's start (0: off) */
-    SGMM_PLAN_N = 10
+    SGMM_PLAN_SEQ_SUM = 10,      /* path-scan episode sums: 0 exact parallel method, 1 sequential chain */
+    SGMM_PLAN_N = 11
 };
 int sgmm_plan_set(int32_t knob, int32_t value);
 int sgmm_plan_get(int32_t knob);

@@ -447,3 +447,38 @@ def test_adversary_small_inventory_ranges(sgmm, oracle, caps):
         f, t = oracle.evaluate(pop[i].numpy(), H, adv[i], s1n[:L], s2n[:L], b[2][:L], b[3][:L], b[4][:L],
                                b[5][:L], b[6][:L], p)
         assert trd[i] == t and fit[i] == f, (caps, L, fit[i], f)
+
+
+@pytest.mark.parametrize("seq", [0, 1], ids=["parallel_sum", "sequential_sum"])
+@pytest.mark.parametrize("n_ep,H,arl", [(128, 16, False), (400, 16, False), (1100, 32, False), (64, 32, True),
+                                          (1500, 32, True)],
+                         ids=["16waves", "4waves", "1wave", "arl_16waves", "arl_4waves"])
+def test_scan_sum_methods_agree(sgmm, oracle, plan, seq, n_ep, H, arl):
+    """The path scans' two episode-sum methods -- the exact parallel binade method
+    and the plain sequential chain (SGMM_PLAN_SEQ_SUM, chosen per launch by
+    scan_seq_sum) -- give the oracle's bits at every scan width, with and without
+    the adversary (whose scan sums 4096-tick segments), on ragged lengths and a
+    wide population (sums near zero and crossing it)."""
+    plan(seq_sum=seq)
+    from sgmm_amd import synthetic
+    lens = np.array([[0, 1, 17, 1023, 1024, 1025, 4095, 4096, 4097, 5000][i % 10] if i < 40 else 700 + (53 * i) % 4300
+                     for i in range(n_ep)], np.int64)
+    P = len(lens)
+    T = int(lens.max())
+    b = synthetic.bundle_510300(T, seed=11)
+    st = synthetic.train_stats(b)
+    pop = synthetic.population(P, H, sigma=0.6, seed=12)
+    adv = synthetic.population(P, 32, sigma=0.3, seed=13) if arl else None
+    ticks = sgmm.TickStore()
+    seg = ticks.add(b, st)
+    ticks.to(DEV)
+    params = sgmm.params_tensor([sgmm.EnvConfig(phi=0.0005, tick_size=0.001)], DEV)
+    eb = sgmm.EpisodeBatch(np.arange(P), np.full(P, ticks.segments[seg][0]), lens, np.zeros(P),
+                           adv=np.arange(P) if arl else None).to(DEV)
+    fit, trd = sgmm.RolloutEngine(DEV).fitness(ticks, eb, params, pop.to(DEV), H, adv.to(DEV) if arl else None)
+    s1n, s2n = sgmm.normalize_signals(b[0], b[1], st)
+    want_f, want_t = oracle.evaluate_batch(pop.numpy(), H, adv.numpy() if arl else None, (s1n, s2n) + tuple(b[2:]),
+                                           np.arange(P), np.arange(P) if arl else None, np.zeros(P), lens,
+                                           np.zeros(P), [oracle.params(phi=0.0005, tick=0.001)], n_threads=8)
+    assert np.array_equal(trd.cpu().numpy(), want_t)
+    assert np.array_equal(fit.cpu().numpy(), want_f)
