@@ -214,6 +214,49 @@ __device__ __forceinline__ void frontier_wave(const EpArrays& ep, int b, int& po
 constexpr uint32_t kKinfoTick = 0xFFFFu;
 __host__ __device__ __forceinline__ uint32_t kinfo_groups(uint32_t k) { return (k >> 20) & 31u; }
 
+// ------------------------------------------------------------------ generation tail
+// A fitness launch can end the generation itself: every workgroup publishes
+// its episode's result (agent-scope release, arrival ticket); the last one to
+// arrive acquires, runs the GA step (tell, validation bookkeeping, sigma
+// decay, history) and resets the ticket.  Saves the separate GA launch.
+struct StepArgs {
+    sgmm_ga_state* st;  // nullptr: no GA step in this launch
+    float* master_mm;
+    float* master_adv;
+    float* best_master;
+    int64_t n_mm, n_adv;
+    uint64_t seed;
+    sgmm_ga_history* history;
+    int32_t hist_cap;
+    int32_t P;          // per population: fitness[0..P) training, fitness[P..2P) validation
+    // several populations: episode e (workgroup e) belongs to population
+    // k = e / pop_eps, whose state / masters / history / key sit at st + k,
+    // master_* + k * n_*, history + k * hist_cap, seeds[k]; its records at
+    // fitness + k * pop_eps.  pop_eps == 0: one population (the whole grid).
+    int32_t pop_eps;
+    const uint64_t* seeds;
+    // 0: the whole boundary (records: P training then P validation results per
+    // population); 1: tell only (the validation of the new master follows in its
+    // own launches); 2: validation bookkeeping, one episode per population
+    // (workgroup k = population k's post-tell master, validation_tail);
+    // 3: the tell's argmax only (the last arriver is a one-wave workgroup whose
+    // master regeneration took ~17 us, profiles/r05_timeline/sc_tr15d.txt) and
+    // 4: its validation launch -- episode k rolls out individual best of
+    // population k (GenomeSrc::use_best) and workgroup k regenerates the master
+    // (all its threads) before the bookkeeping
+    int32_t mode;
+};
+
+// The episode's fitness record, stored write-through (sc1) by ONE lane of
+// the workgroup: the hand-off to the generation tail needs no release fence.
+__device__ __forceinline__ void store_record(double* fitness, int32_t* trades, int e, double f,
+                                             int32_t t) {
+    typedef __attribute__((address_space(1))) double gdouble;
+    typedef __attribute__((address_space(1))) int32_t gint;
+    __hip_atomic_store((gdouble*)(fitness + e), f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((gint*)(trades + e), t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ------------------------------------------------------------------ frontier kernel launch
 struct FrontierArgs {
     sgmm_ticks tk;
@@ -232,7 +275,30 @@ struct FrontierArgs {
     // its chunks have at most kSpillTicks ticks left
     uint32_t* wspill;
     uint32_t spill_budget;
+    // fused path scan (k_policy_frontier<..., FS = true>): each walk sums its own
+    // chunk group; of an episode walked in two groups, group 0 hands the chain on
+    // through handoff[e] (or group 1 hands its rows over), hstate[e] the arrival
+    // word (zero before the launch, reset by the wave that ends the chain); the
+    // chain's last wave stores the record in fitness / trades, and the last record
+    // of a population runs the generation tail (step: none or mode 3)
+    double* fitness;
+    int32_t* trades;
+    struct FusedHandoff* handoff;
+    uint32_t* hstate;
+    int32_t n_eps;
+    StepArgs step;
 };
+// group 0's chain state for group 1: the sum after its chunks, the state the path
+// enters chunk 64 in (bits 0-7) and the trades so far (bits 8-31)
+struct FusedHandoff {
+    double S;
+    uint32_t st_tr;
+    uint32_t pad;
+};
+// fused path scan: a frontier walk's LDS holds a 512-tick window of the sum and
+// its group's 64 start states / merge infos; at most two groups per episode
+constexpr int kFusedWin = 512;
+constexpr int kFusedMaxGroups = 2;
 constexpr int kSpillTicks = 64;  // a spilled chunk's remaining ticks fit one wave (lane = tick)
 
 // wave_map_scan within segments of SEG = 16, 32 or 64 lanes
@@ -249,6 +315,7 @@ __device__ __forceinline__ uint64_t wave_map_scan_seg(uint64_t m) {
 // launches the frontier kernel for hidden = 16 / 32 and nsi inventory states
 // (sgmm_frontier.hip): grid = episodes x ep.ngrp waves
 // ls: waves per 64-chunk group (1, 2 or 4; the grid is n_waves x ls)
+// fa.fitness != nullptr: the fused path scan (ls = 1, ep.ngrp <= kFusedMaxGroups)
 int launch_policy_frontier(int hidden, int nsi, unsigned n_waves, int ls, hipStream_t s, const FrontierArgs& fa);
 // completes the chunks of the walks that spilled (fa.wspill) tick-parallel; a
 // fixed grid (graph-capturable) that exits at once when no walk spilled

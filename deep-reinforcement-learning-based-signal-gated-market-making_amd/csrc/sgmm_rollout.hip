@@ -1411,38 +1411,7 @@ __device__ __forceinline__ double exact_sum_window(const double* sel, int n, dou
     return L.S;
 }
 
-// ------------------------------------------------------------------ generation tail
-// A fitness launch can end the generation itself: every workgroup publishes
-// its episode's result (agent-scope release, arrival ticket); the last one to
-// arrive acquires, runs the GA step (tell, validation bookkeeping, sigma
-// decay, history) and resets the ticket.  Saves the separate GA launch.
-struct StepArgs {
-    sgmm_ga_state* st;  // nullptr: no GA step in this launch
-    float* master_mm;
-    float* master_adv;
-    float* best_master;
-    int64_t n_mm, n_adv;
-    uint64_t seed;
-    sgmm_ga_history* history;
-    int32_t hist_cap;
-    int32_t P;          // per population: fitness[0..P) training, fitness[P..2P) validation
-    // several populations: episode e (workgroup e) belongs to population
-    // k = e / pop_eps, whose state / masters / history / key sit at st + k,
-    // master_* + k * n_*, history + k * hist_cap, seeds[k]; its records at
-    // fitness + k * pop_eps.  pop_eps == 0: one population (the whole grid).
-    int32_t pop_eps;
-    const uint64_t* seeds;
-    // 0: the whole boundary (records: P training then P validation results per
-    // population); 1: tell only (the validation of the new master follows in its
-    // own launches); 2: validation bookkeeping, one episode per population
-    // (workgroup k = population k's post-tell master, validation_tail);
-    // 3: the tell's argmax only (the last arriver is a one-wave workgroup whose
-    // master regeneration took ~17 us, profiles/r05_timeline/sc_tr15d.txt) and
-    // 4: its validation launch -- episode k rolls out individual best of
-    // population k (GenomeSrc::use_best) and workgroup k regenerates the master
-    // (all its threads) before the bookkeeping
-    int32_t mode;
-};
+
 
 // LDS bytes the tail needs (aliased onto the kernel's dynamic LDS)
 static inline size_t step_lds_bytes(int threads, const StepArgs& sa) {
@@ -1450,15 +1419,6 @@ static inline size_t step_lds_bytes(int threads, const StepArgs& sa) {
            sizeof(float) * (size_t)(sa.n_mm + (sa.master_adv ? sa.n_adv : 0));
 }
 
-// The episode's fitness record, stored write-through (sc1) by ONE lane of
-// the workgroup: the hand-off to the generation tail needs no release fence.
-__device__ __forceinline__ void store_record(double* fitness, int32_t* trades, int e, double f,
-                                             int32_t t) {
-    typedef __attribute__((address_space(1))) double gdouble;
-    typedef __attribute__((address_space(1))) int32_t gint;
-    __hip_atomic_store((gdouble*)(fitness + e), f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store((gint*)(trades + e), t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Thread 0 stored the workgroup's record with store_record.  It drains the
 // stores, takes an arrival ticket (agent-scope atomic); the workgroup that
@@ -2272,6 +2232,10 @@ static size_t ws_wslots(int32_t n) { return align256((size_t)n * 64 * sizeof(uin
 // u32 wspill[n * 64]: per frontier wave (<= 16 groups x 4 waves per episode) the
 // tick offset at which it spilled, 0 if it did not
 static size_t ws_wspill(int32_t n) { return align256((size_t)n * 64 * sizeof(uint32_t)); }
+// the fused scan's per-episode arrival words and chain hand-offs (FrontierArgs::hstate, handoff)
+static size_t ws_arrive(int32_t n) {
+    return align256((size_t)n * sizeof(uint32_t)) + align256((size_t)n * sizeof(FusedHandoff));
+}
 
 // The workspace of a batch with n_inventory inventory values, with or
 // without the adversary (then 4 * n_inventory states: inventory x previous
@@ -2282,7 +2246,7 @@ static size_t rollout_ws_bytes(int32_t n_episodes, int64_t total_steps, int32_t 
     if (arl)  // fill codes, per-state planes rew[state * rs + row]
         return ws_fills(total_steps) + (size_t)rew_stride(total_steps, n_episodes, true) * (size_t)(4 * nsi) * sizeof(double);
     return ws_cmaps(n_episodes, total_steps) + ws_ctr(n_episodes, total_steps) + ws_kinfo(n_episodes) +
-           ws_wslots(n_episodes) + ws_wspill(n_episodes) +
+           ws_wslots(n_episodes) + ws_wspill(n_episodes) + ws_arrive(n_episodes) +
            (size_t)rew_stride(total_steps, n_episodes, false) * (size_t)nsi * sizeof(double);
 }
 
@@ -2454,6 +2418,31 @@ static bool scan_seq_sum(int nt, bool arl, bool validation) {
     return !arl && nt <= 256;
 }
 
+// The path scan fused into the frontier launch (k_policy_frontier<..., FS>): each
+// walk sums its own episode (the sequential chain) while the launch's longer walks
+// still run, and the last record of a population runs the tell -- no separate
+// scan launch.  Where it applies: one wave per walk, <= kFusedMaxGroups groups, no
+// spill, no tail or the tell's argmax (mode 3), not where the parallel sum is forced.
+// The default takes it for launches of whole walks only (round 6, profiles/r06_fused/,
+// per generation: config 5 1.344-1.360 -> 1.327-1.332 ms, its 1-of-2 shard
+// 0.789-0.794 -> 0.759-0.761, 1-of-4 0.489-0.490 -> 0.469-0.471); with halves the
+// chain hand-offs and the in-kernel sums on SIMDs shared with walks cost more than
+// the separate scan (config 3 0.639-0.641 -> 0.646-0.650, the 1-of-8 shard 0.333 ->
+// 0.372 ms).  SGMM_PLAN_FUSED_SCAN forces it off (0) or on where it applies (1).
+static bool fused_scan_plan(const FrontierPlan& plan, uint32_t spill, const StepArgs& step, bool vt) {
+    const int v = plan_value(SGMM_PLAN_FUSED_SCAN);
+    if (v == 0 || vt || spill || plan.ls != 1 || plan.gmax > kFusedMaxGroups) return false;
+    if (plan_value(SGMM_PLAN_SEQ_SUM) == 0) return false;  // the parallel method forced
+    if (step.st && step.mode != 3) return false;
+    return v == 1 || plan.gmax == 1;
+}
+
+// zero n words (the fused scan's arrival counters)
+__global__ __launch_bounds__(1024) void k_zero_u32(uint32_t* __restrict__ p, int32_t n) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) p[i] = 0u;
+}
+
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
 // per walk, whole populations of equal-length episodes, the caller's writable
 // walk order (sgmm_populations::walk_order)
@@ -2492,6 +2481,7 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
     uint32_t* kinfo = nullptr;
     uint32_t* wslots = nullptr;
     uint32_t* wspill = nullptr;
+    uint32_t* arrive = nullptr;
     double* rew;
     if (arl) {
         fills = reinterpret_cast<uint64_t*>(w);
@@ -2502,8 +2492,10 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         ctr = reinterpret_cast<uint64_t*>(w + a);
         kinfo = reinterpret_cast<uint32_t*>(w + a + b);
         wslots = reinterpret_cast<uint32_t*>(w + a + b + ws_kinfo(eps->n));
-        wspill = reinterpret_cast<uint32_t*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n));
-        rew = reinterpret_cast<double*>(w + a + b + ws_kinfo(eps->n) + ws_wslots(eps->n) + ws_wspill(eps->n));
+        const size_t c = a + b + ws_kinfo(eps->n) + ws_wslots(eps->n);
+        wspill = reinterpret_cast<uint32_t*>(w + c);
+        arrive = reinterpret_cast<uint32_t*>(w + c + ws_wspill(eps->n));
+        rew = reinterpret_cast<double*>(w + c + ws_wspill(eps->n) + ws_arrive(eps->n));
     }
     EpArrays ep = ep_arrays(eps, arl);
     const ReorderJob* rj_fold = nullptr;
@@ -2538,10 +2530,26 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
             rj_done = true;
         }
     }
+    const uint32_t spill = fr ? spill_budget(eps, plan) : 0u;
+    const bool fused = fr && eps->max_len > 0 && fused_scan_plan(plan, spill, step, vt);
     if (fr && eps->max_len > 0) {
+        FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
+                        kinfo, rew, wslots, wspill, spill};
+        if (fused) {
+            fa.fitness = fitness;
+            fa.trades = trades;
+            fa.hstate = arrive;
+            fa.handoff = reinterpret_cast<FusedHandoff*>(reinterpret_cast<char*>(arrive) + align256((size_t)eps->n * sizeof(uint32_t)));
+            fa.n_eps = eps->n;
+            fa.step = step;
+            // the arrival words start at zero (the wave that ends an episode's chain
+            // resets its word; a workspace is not zeroed before its first use).  A kernel,
+            // not hipMemsetAsync: replayed after other launches, a captured memset
+            // node left stale values here (tools/diag_fused2.py, round 6)
+            if (plan.gmax > 1)
+                SGMM_LAUNCH(k_zero_u32, dim3((eps->n + 1023) / 1024), dim3(1024), 0, s, arrive, eps->n);
+        }
         ProfScope prof(vt ? "val_policy_frontier" : "policy_frontier", s);
-        const FrontierArgs fa{*ticks, ep, params, src, eps->inv_min, nsi, cmaps, reinterpret_cast<uint32_t*>(ctr),
-                              kinfo, rew, wslots, wspill, spill_budget(eps, plan)};
         if (int rc = launch_policy_frontier(hidden, nsi, (unsigned)plan.waves, plan.ls, s, fa)) return rc;
         if (fa.spill_budget) {
             ProfScope prof2(vt ? "val_frontier_spill" : "frontier_spill", s);
@@ -2573,8 +2581,9 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         }
         SGMM_LAUNCHED();
     }
-    ProfScope prof(vt ? "val_path_scan" : "path_scan", s);
-    if (arl) {
+    if (fused) {
+        // the frontier launch summed every episode and ran the tail
+    } else if (ProfScope prof(vt ? "val_path_scan" : "path_scan", s); arl) {
         // 16-wave workgroups while one per CU fits (a 4096-tick segment is one
         // exact-sum window), 4-wave ones beyond
         const int nt = eps->n <= kScanArlAt1024 ? kScanThreads : kScanBlock;

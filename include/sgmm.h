@@ -494,7 +494,8 @@ enum {
     SGMM_PLAN_REORDER_WEIGHTS = 8, /* walk-order scores: whole << 8 | split */
     SGMM_PLAN_SPILL = 9,         /* frontier spill deadline, us after a walk's start (0: off) */
     SGMM_PLAN_SEQ_SUM = 10,      /* path-scan episode sums: 0 exact parallel method, 1 sequential chain */
-    SGMM_PLAN_N = 11
+    SGMM_PLAN_FUSED_SCAN = 11,   /* frontier launches: 0 separate path scan, 1 scans fused into the walks */
+    SGMM_PLAN_N = 12
 };
 int sgmm_plan_set(int32_t knob, int32_t value);
 int sgmm_plan_get(int32_t knob);

@@ -75,9 +75,11 @@ def test_argument_errors_need_no_gpu(sgmm):
     # episodes, the default rule's cap: u64 map, u32[8] counts, u32 merge info) (planes:
     # 1000 ticks + 4 x (256 G + 16) padding rows of the frontier layout -- 128-byte aligned
     # episode blocks -- rounded to 32: 9280); u32 slots per frontier wave (64 per episode);
-    # u32 spill entries per frontier wave (64 per episode: <= 16 groups x 4 waves)
+    # u32 spill entries per frontier wave (64 per episode: <= 16 groups x 4 waves); the
+    # fused scan's u32 arrival words and 16-byte chain hand-offs (one each per episode,
+    # 256-aligned)
     assert L.sgmm_rollout_workspace_size(4, 1000, 5) == (4 * 512 * 8 + 4 * 512 * 32 + 4 * 512 * 4
-                                                         + 4 * 64 * 4 + 4 * 64 * 4 + 5 * 9280 * 8)
+                                                         + 4 * 64 * 4 + 4 * 64 * 4 + 256 + 256 + 5 * 9280 * 8)
     # bundle builder: group starts (i32) + times (i64), 256-aligned, + 7 f64 stats per tick
     assert L.sgmm_event_bars_workspace_size(1000) == 4096 + 8192 + 56000
     rc = L.sgmm_event_bars_build(None, None, None, 0, None)
@@ -115,7 +117,8 @@ def test_gpu_entry_points_fail_loudly_without_gpu(sgmm):
 PLAN_ENV = {"SGMM_TABLE_PATH": "frontier", "SGMM_FRONTIER_NW": "3", "SGMM_FRONTIER_LS": "2",
             "SGMM_FRONTIER_TAIL": "0", "SGMM_FRONTIER_FOUR": "0", "SGMM_FRONTIER_MIN_EPS": "4",
             "SGMM_TABLE_SP": "1", "SGMM_SCAN_THREADS": "256", "SGMM_REORDER_WEIGHTS": "5,5",
-            "SGMM_FRONTIER_SPILL": "0", "SGMM_FRONTIER_REORDER": "0", "SGMM_SEQ_SUM": "1"}
+            "SGMM_FRONTIER_SPILL": "0", "SGMM_FRONTIER_REORDER": "0", "SGMM_SEQ_SUM": "1",
+            "SGMM_FUSED_SCAN": "0"}
 
 
 def test_shipped_library_reads_no_plan_environment(sgmm):
@@ -132,8 +135,8 @@ def test_shipped_library_reads_no_plan_environment(sgmm):
         assert name.encode() not in blob, name
     assert b"getenv" not in blob
     code = ("import sgmm_pkg; sgmm_pkg.load(); from sgmm_amd import _lib; L = _lib.load(); "
-            "print([L.sgmm_plan_get(k) for k in range(11)], L.sgmm_rollout_workspace_bytes(2560, 2560 * 4560, 5, 0), "
-            "L.sgmm_plan_get(11))")
+            "print([L.sgmm_plan_get(k) for k in range(12)], L.sgmm_rollout_workspace_bytes(2560, 2560 * 4560, 5, 0), "
+            "L.sgmm_plan_get(12))")
     env = dict(os.environ)
     clean = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
                            check=True).stdout.split("\n")[-2]
@@ -141,7 +144,7 @@ def test_shipped_library_reads_no_plan_environment(sgmm):
     dirty = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
                            check=True).stdout.split("\n")[-2]
     assert dirty == clean
-    assert clean.startswith("[" + ", ".join(["-1"] * 11) + "]")
+    assert clean.startswith("[" + ", ".join(["-1"] * 12) + "]")
     assert clean.endswith(str(-2**31))  # unknown knob
 
 

@@ -280,3 +280,45 @@ def test_frontier_lane_split(sgmm, oracle, plan, ls, nw, H):
         fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=71, caps=caps, sigma=0.5)
         assert np.array_equal(trd, wt), caps
         assert np.array_equal(fit, wf), caps
+
+
+@pytest.mark.parametrize("fused", [0, 1], ids=["separate_scan", "fused_scan"])
+@pytest.mark.parametrize("groups", [1, 2, 3], ids=["whole", "halves", "thirds"])
+@pytest.mark.parametrize("H", [16, 32])
+def test_frontier_fused_scan(sgmm, oracle, plan, fused, groups, H):
+    """The path scan fused into the frontier launch (k_policy_frontier<..., FS>):
+    each walk sums its own chunk group; of an episode walked in halves, group 0
+    hands the chain (sum, state, trades) on to group 1, or continues over group
+    1's handed-over rows when group 1 finished first.  Against the separate scan
+    launch and the oracle, bit for bit: empty and one-tick episodes (group 0
+    stores the record without a walk), halves whose second group has no chunks,
+    ragged lengths across the 512-tick windows; more than two groups keep the
+    separate scan."""
+    from sgmm_amd import _lib
+    plan(policy_path="frontier", groups=groups, fused_scan=fused)
+    lens = [0, 1, 5, 64, 257, 511, 512, 513, 4560, 0, 9001, 3600, 700, 2]
+    _lib.profile_read()
+    _lib.profile_enable(True)
+    try:
+        fit, trd, wf, wt = _run(sgmm, oracle, lens, H, seed=53, sigma=0.4)
+        kinds = _lib.profile_read()
+    finally:
+        _lib.profile_enable(False)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
+    assert fit[0] == -50.0 and trd[0] == 0 and fit[9] == -50.0
+    assert "policy_frontier" in kinds
+    assert ("path_scan" in kinds) == (fused == 0 or groups > 2)
+
+
+@pytest.mark.parametrize("seed", [61, 62, 63])
+def test_frontier_fused_scan_handoff_both_ways(sgmm, oracle, plan, seed):
+    """Halves of very different weight: wide policies (paths that never merge) next
+    to narrow ones, so that in some episodes group 0 finishes last (and continues
+    over group 1's handed-over rows) and in others group 1 does (and continues
+    group 0's chain) -- 1 200 episodes, bit-exact."""
+    plan(policy_path="frontier", groups=2, fused_scan=1)
+    lens = 1000 + (np.arange(1200) * 53) % 3700
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=seed, sigma=1.0, nan_frac=0.02)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
