@@ -218,7 +218,7 @@ def profile_read(max_kinds: int = 32) -> dict:
 # launch-plan overrides (include/sgmm.h SGMM_PLAN_*): tests and A/B experiments
 PLAN_KNOBS = {"policy_path": 0, "groups": 1, "lane_split": 2, "tail": 3, "four": 4, "min_eps": 5,
               "table_sp": 6, "scan_threads": 7, "reorder_weights": 8, "spill": 9, "seq_sum": 10,
-              "fused_scan": 11}
+              "fused_scan": 11, "lanes_scan": 12}
 POLICY_PATHS = {"auto": -1, "frontier": 1, "table": 2, "valu": 3}
 
 

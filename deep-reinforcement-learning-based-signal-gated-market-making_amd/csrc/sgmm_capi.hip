@@ -60,6 +60,7 @@ void plan_init() {
     g_plan[SGMM_PLAN_SPILL].store(env("SGMM_FRONTIER_SPILL"));
     g_plan[SGMM_PLAN_SEQ_SUM].store(env("SGMM_SEQ_SUM"));
     g_plan[SGMM_PLAN_FUSED_SCAN].store(env("SGMM_FUSED_SCAN"));
+    g_plan[SGMM_PLAN_LANES_SCAN].store(env("SGMM_LANES_SCAN"));
     if (const char* v = std::getenv("SGMM_REORDER_WEIGHTS")) {
         unsigned a = 0, b = 0;
         if (std::sscanf(v, "%u,%u", &a, &b) == 2 && a > 0 && b > 0 && a < 64 && b < 64)

@@ -1692,6 +1692,200 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
 }
 
 
+// ------------------------------------------------------------------ path scan, W episodes per workgroup
+// The frontier path scan for many episodes, the sums as sequential chains: wave w
+// of the workgroup takes episode e0 + w through the scan's first two phases (chunk
+// start states and trades; the rewards of its path, kLanesWin ticks per window,
+// into LDS row w, padded with -0.0), and wave 0 adds the W windows, lane w episode
+// e0 + w, one dependent v_add_f64 advancing all W chains.  The one-wave scan ran
+// one chain per wave on all 64 lanes: with 2-3 scans per SIMD its float64 adds
+// shared the vector pipe (trained config 3: ~20 cycles per tick and episode,
+// against ~10 for a lone chain, tools/mb_trained_timeline.py SCAN=1).  x + -0.0 == x
+// for every x, so the padding leaves each episode's sum its reference-order chain.
+// The generation tail: the workgroup's W records, one arrival of W (the tell's
+// argmax, StepArgs mode 3, when its last population record arrives).
+// W and the window measured (profiles/r06_lanes/, scan of config 3 / of config 5's
+// 1-of-8 shard): W = 16 57.8 / 40.5 us, 8 59.5 / 33.9, 4 55.5 / 31.1, 2 53.5 / 33.5;
+// 1024-tick windows 56.5-59.6 / 33.8 (one episode per wave: 72.2 / 37.5)
+#ifndef SGMM_LANES_W
+#define SGMM_LANES_W 4
+#endif
+constexpr int kLanesW = SGMM_LANES_W;       // episodes per workgroup
+#ifndef SGMM_LANES_WIN
+#define SGMM_LANES_WIN 512
+#endif
+constexpr int kLanesWin = SGMM_LANES_WIN;   // ticks per window
+constexpr int kLanesPitch = kLanesWin + 2;  // doubles per LDS row (16-byte bank offset per row)
+static size_t lanes_scan_lds(int ngrp) {
+    return (size_t)kLanesW * kLanesPitch * sizeof(double) +
+           (size_t)kLanesW * kFrontierLanes * ngrp * (sizeof(uint32_t) + 1) + 64;
+}
+template <int NSM>
+__global__ __launch_bounds__(kWave * kLanesW) void k_path_scan_lanes(
+    EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, const uint64_t* __restrict__ cmaps,
+    const uint32_t* __restrict__ ctr32, const uint32_t* __restrict__ kinfo, const double* __restrict__ rew,
+    double* __restrict__ fitness, int32_t* __restrict__ trades_out, StepArgs step, int32_t n) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const int nw = ep.ngrp;
+    double* win = reinterpret_cast<double*>(lds);  // [kLanesW][kLanesPitch]
+    uint32_t* kin_all = reinterpret_cast<uint32_t*>(win + kLanesW * kLanesPitch);
+    uint8_t* start_all = reinterpret_cast<uint8_t*>(kin_all + kLanesW * kFrontierLanes * nw);
+    __shared__ int32_t red_s[kLanesW];
+    __shared__ int32_t len_s[kLanesW];
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & (kWave - 1));
+    const int e0 = (int)blockIdx.x * kLanesW, e = e0 + w;
+    SGMM_STAMP(blockIdx.x, 0);
+#ifdef SGMM_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][12] = 0;
+#endif
+    const bool has = e < n;
+    const int32_t T = has ? ep.len[e] : 0;
+    uint32_t* kin = kin_all + w * kFrontierLanes * nw;
+    uint8_t* start = start_all + w * kFrontierLanes * nw;
+    double* row = win + w * kLanesPitch;
+    // 1. (wave w) chunk start states and the trades along the path
+    const int64_t cb = frontier_rec(has ? e : 0, nw, 0);
+    const int nwe = T > 0 ? (int)kinfo_groups(kinfo[cb]) : 1;
+    const int CL = frontier_len(T, nwe);
+    const int nch = T > 0 ? (T + CL - 1) / CL : 0;
+    {
+        uint32_t s = (uint32_t)(-inv_min);
+        int tr = 0;
+        for (int c0 = 0; c0 < nch; c0 += kWave) {
+            const int c = c0 + lane;
+            const uint64_t m = c < nch ? cmaps[cb + c] : kIdentityMap;
+            const uint64_t inc = wave_map_scan(m);
+            uint64_t excl = shfl_up_u64(inc, 1);
+            if (lane == 0) excl = kIdentityMap;
+            const uint32_t st = map_get(excl, s);
+            if (c < nch) {
+                start[c] = (uint8_t)st;
+                kin[c] = kinfo[cb + c];
+                tr += (int)ctr32[(cb + c) * 8 + st];
+            }
+            s = map_get(readlane64(inc, kWave - 1), s);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, kWave);
+        if (lane == 0) {
+            red_s[w] = tr;
+            len_s[w] = T;
+        }
+    }
+    __syncthreads();
+    SGMM_STAMP(blockIdx.x, 1);
+    int tmax = 0;
+#pragma unroll
+    for (int i = 0; i < kLanesW; ++i) tmax = max(tmax, len_s[i]);
+    // 2. windows: every wave gathers its episode's next window while wave 0 adds
+    const int64_t base = frontier_base(has ? ep.step_off[e] : 0, has ? e : 0, nw);
+    constexpr int kG = kLanesWin / (4 * kWave);
+    double r[kG][4];
+    auto gather = [&](int w0) {
+        const int cnt = min(kLanesWin, T - w0);  // <= 0 past the episode's end
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int i0 = (q * kWave + lane) * 4;
+            if (i0 < cnt) {
+                const int c = (w0 + i0) / CL, u = w0 + i0 - c * CL;
+                const uint32_t ki = kin[c];
+                const int kc = (int)(ki & kKinfoTick);
+                const int64_t pst = start[c], pp0 = ki >> 29;
+                const int64_t rb = base + (int64_t)(c / kFrontierLanes) * CL * kFrontierLanes +
+                                   frontier_row(u, c % kFrontierLanes);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int jj = min(j, cnt - 1 - i0);
+                    r[q][j] = rew[(u + jj >= kc ? pp0 : pst) * ep.rs + rb + (int64_t)jj * kFrontierLanes];
+                }
+            }
+        }
+    };
+    gather(0);
+    double S = 0.0;  // wave 0, lane v < kLanesW: episode e0 + v
+    const double* mine = win + min(lane, kLanesW - 1) * kLanesPitch;
+    for (int w0 = 0; w0 < tmax; w0 += kLanesWin) {
+        const int cnt = T - w0;
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+            const int i0 = (q * kWave + lane) * 4;
+            double2 a, b;
+            a.x = i0 < cnt ? r[q][0] : -0.0;
+            a.y = i0 + 1 < cnt ? r[q][1] : -0.0;
+            b.x = i0 + 2 < cnt ? r[q][2] : -0.0;
+            b.y = i0 + 3 < cnt ? r[q][3] : -0.0;
+            *reinterpret_cast<double2*>(row + i0) = a;
+            *reinterpret_cast<double2*>(row + i0 + 2) = b;
+        }
+        __syncthreads();
+#ifdef SGMM_STAMPS
+        if (w0 == 0) SGMM_STAMP(blockIdx.x, 2);
+        unsigned long long ch0;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch0)::"memory");
+#endif
+        if (w0 + kLanesWin < T) gather(w0 + kLanesWin);
+        if (w == 0) {
+            // this window's length over the workgroup's episodes
+            const int m = min(kLanesWin, tmax - w0);
+            const double2* p = reinterpret_cast<const double2*>(mine);
+            int i = 0;
+            for (; i + 32 <= m; i += 32) {
+                double2 v[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) v[j] = p[i / 2 + j];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    S += v[j].x;
+                    S += v[j].y;
+                }
+            }
+            for (; i < m; ++i) S += mine[i];
+#ifdef SGMM_STAMPS
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            unsigned long long ch1;
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch1)::"memory");
+            if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][12] += ch1 - ch0;
+#endif
+        }
+        __syncthreads();  // the windows are read before the next ones are written
+    }
+    SGMM_STAMP(blockIdx.x, 3);
+    // 3. records (wave 0, lane v: episode e0 + v) and the generation tail
+    if (w == 0) {
+        const int nv = min(kLanesW, n - e0);
+        if (lane < nv) {
+            const int ev = e0 + lane;
+            const int32_t tr = red_s[lane];
+            double total = S;
+            if (tr == 0) total -= params[ep.param[ev]].idle_penalty;  // drl_engine.py:64-65
+            store_record(fitness, trades_out, ev, total, tr);
+        }
+        if (step.st) {
+            const int n_eps = step.pop_eps > 0 ? step.pop_eps : n;
+            const int k = step.pop_eps > 0 ? e0 / step.pop_eps : 0;
+            int last = 0;
+            if (lane == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's record stores
+                last = __hip_atomic_fetch_add(&step.st[k].arrivals, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                       n_eps - nv;
+            }
+            if (__shfl(last, 0, kWave)) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler order only: loads after the ticket
+                sgmm_ga_state* st = step.st + k;
+                tell_wave<true, false>(st, fitness + (int64_t)k * n_eps, trades_out + (int64_t)k * n_eps, step.P,
+                                       step.master_mm + (int64_t)k * step.n_mm,
+                                       step.master_adv ? step.master_adv + (int64_t)k * step.n_adv : nullptr,
+                                       step.n_mm, step.n_adv, step.seeds ? step.seeds[k] : step.seed,
+                                       step.history ? step.history + (int64_t)k * step.hist_cap : nullptr,
+                                       step.hist_cap);
+                if (lane == 0) st->arrivals = 0;
+            }
+        }
+    }
+    SGMM_STAMP(blockIdx.x, 4);
+}
+
+
 // ------------------------------------------------------------------ ordered sum (standalone)
 // init + x[0] + x[1] + ... in sequential float64 order, one workgroup.
 __global__ __launch_bounds__(kScanThreads) void k_ordered_sum(const double* __restrict__ x, int64_t n,
@@ -2443,6 +2637,19 @@ __global__ __launch_bounds__(1024) void k_zero_u32(uint32_t* __restrict__ p, int
     if (i < n) p[i] = 0u;
 }
 
+// The frontier path scan with kLanesW episodes per workgroup and their chains in
+// the lanes of one wave (k_path_scan_lanes): where the one-wave scan would run the
+// sequential chain, with no tail or the tell's argmax (mode 3) and populations of
+// whole workgroups (config 3: scan 72 -> 55.5 us, 0.627-0.639 -> 0.605-0.612 ms
+// per generation; config 5's 1-of-8 shard 37.5 -> 31.1 us).  SGMM_PLAN_LANES_SCAN forces it off (0) or on where it applies (1).
+static bool lanes_scan(int nt, bool seq, const StepArgs& step, int32_t pop_eps) {
+    const int v = plan_value(SGMM_PLAN_LANES_SCAN);
+    if (v == 0 || !seq || (step.st && step.mode != 3)) return false;
+    if (step.st && step.pop_eps > 0 && step.pop_eps % kLanesW != 0) return false;
+    (void)pop_eps;
+    return v == 1 || nt == kWave;
+}
+
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
 // per walk, whole populations of equal-length episodes, the caller's writable
 // walk order (sgmm_populations::walk_order)
@@ -2604,10 +2811,19 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         // instead of idling the CU (A/B on MI355X: P=64 / 256 / 1024 / 4096)
         const int nt = scan_threads(eps->n);
         ep.seq_sum = scan_seq_sum(nt, false, vt) ? 1 : 0;
-        size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double);  // the window
-        if (fr) lds += (size_t)5 * kFrontierLanes * ep.ngrp;  // chunk start states + merge info
-        if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
-        if (fr) {
+        if (fr && lanes_scan(nt, ep.seq_sum != 0, step, src.pop_eps)) {
+            const size_t lds = lanes_scan_lds(ep.ngrp);
+            const dim3 grid((eps->n + kLanesW - 1) / kLanesW), block(kWave * kLanesW);
+            if (nsi <= 5)
+                SGMM_LAUNCH(k_path_scan_lanes<5>, grid, block, lds, s, ep, params, eps->inv_min, cmaps,
+                            reinterpret_cast<const uint32_t*>(ctr), kinfo, rew, fitness, trades, step, eps->n);
+            else
+                SGMM_LAUNCH(k_path_scan_lanes<8>, grid, block, lds, s, ep, params, eps->inv_min, cmaps,
+                            reinterpret_cast<const uint32_t*>(ctr), kinfo, rew, fitness, trades, step, eps->n);
+        } else if (size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double) +  // the window
+                                (fr ? (size_t)5 * kFrontierLanes * ep.ngrp : 0);  // chunk start states + merge info
+                   fr) {
+            if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
             if (nsi <= 5)
                 launch_path_scan<5, true>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
                                           fitness, trades, step);
@@ -2615,9 +2831,11 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
                 launch_path_scan<8, true>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
                                           fitness, trades, step);
         } else if (nsi <= 5) {
+            if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
             launch_path_scan<5, false>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
                                        fitness, trades, step);
         } else {
+            if (step.st) lds = std::max(lds, step_lds_bytes(nt, step));
             launch_path_scan<8, false>(nt, eps->n, lds, s, ep, params, eps->inv_min, cmaps, ctr, kinfo, rew,
                                        fitness, trades, step);
         }

@@ -118,7 +118,7 @@ PLAN_ENV = {"SGMM_TABLE_PATH": "frontier", "SGMM_FRONTIER_NW": "3", "SGMM_FRONTI
             "SGMM_FRONTIER_TAIL": "0", "SGMM_FRONTIER_FOUR": "0", "SGMM_FRONTIER_MIN_EPS": "4",
             "SGMM_TABLE_SP": "1", "SGMM_SCAN_THREADS": "256", "SGMM_REORDER_WEIGHTS": "5,5",
             "SGMM_FRONTIER_SPILL": "0", "SGMM_FRONTIER_REORDER": "0", "SGMM_SEQ_SUM": "1",
-            "SGMM_FUSED_SCAN": "0"}
+            "SGMM_FUSED_SCAN": "0", "SGMM_LANES_SCAN": "0"}
 
 
 def test_shipped_library_reads_no_plan_environment(sgmm):
@@ -135,8 +135,8 @@ def test_shipped_library_reads_no_plan_environment(sgmm):
         assert name.encode() not in blob, name
     assert b"getenv" not in blob
     code = ("import sgmm_pkg; sgmm_pkg.load(); from sgmm_amd import _lib; L = _lib.load(); "
-            "print([L.sgmm_plan_get(k) for k in range(12)], L.sgmm_rollout_workspace_bytes(2560, 2560 * 4560, 5, 0), "
-            "L.sgmm_plan_get(12))")
+            "print([L.sgmm_plan_get(k) for k in range(13)], L.sgmm_rollout_workspace_bytes(2560, 2560 * 4560, 5, 0), "
+            "L.sgmm_plan_get(13))")
     env = dict(os.environ)
     clean = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
                            check=True).stdout.split("\n")[-2]
@@ -144,7 +144,7 @@ def test_shipped_library_reads_no_plan_environment(sgmm):
     dirty = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True,
                            check=True).stdout.split("\n")[-2]
     assert dirty == clean
-    assert clean.startswith("[" + ", ".join(["-1"] * 12) + "]")
+    assert clean.startswith("[" + ", ".join(["-1"] * 13) + "]")
     assert clean.endswith(str(-2**31))  # unknown knob
 
 
