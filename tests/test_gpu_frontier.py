@@ -313,10 +313,11 @@ def test_frontier_fused_scan(sgmm, oracle, plan, fused, groups, H):
 
 @pytest.mark.parametrize("seed", [61, 62, 63])
 def test_frontier_fused_scan_handoff_both_ways(sgmm, oracle, plan, seed):
-    """Halves of very different weight: wide policies (paths that never merge) next
-    to narrow ones, so that in some episodes group 0 finishes last (and continues
-    over group 1's handed-over rows) and in others group 1 does (and continues
-    group 0's chain) -- 1 200 episodes, bit-exact."""
+    """Halves of very different weight: wide policies (paths that rarely merge) and
+    ragged lengths, 1 200 episodes whose two groups finish in either order -- group
+    0 last (it continues over group 1's handed-over rows) or group 1 last (it
+    continues group 0's chain); which order each episode takes is not observed
+    here, only that every result is bit-exact."""
     plan(policy_path="frontier", groups=2, fused_scan=1)
     lens = 1000 + (np.arange(1200) * 53) % 3700
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=seed, sigma=1.0, nan_frac=0.02)
