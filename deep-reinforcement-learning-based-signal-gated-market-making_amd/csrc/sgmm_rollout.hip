@@ -1734,6 +1734,7 @@ __global__ __launch_bounds__(kWave * kLanesW) void k_path_scan_lanes(
     __shared__ int32_t len_s[kLanesW];
     const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & (kWave - 1));
     const int e0 = (int)blockIdx.x * kLanesW, e = e0 + w;
+    constexpr int wc = 0;  // the chain wave (rotating it over the SIMDs measured no different)
     SGMM_STAMP(blockIdx.x, 0);
 #ifdef SGMM_STAMPS
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][12] = 0;
@@ -1824,7 +1825,7 @@ __global__ __launch_bounds__(kWave * kLanesW) void k_path_scan_lanes(
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ch0)::"memory");
 #endif
         if (w0 + kLanesWin < T) gather(w0 + kLanesWin);
-        if (w == 0) {
+        if (w == wc) {
             // this window's length over the workgroup's episodes
             const int m = min(kLanesWin, tmax - w0);
             const double2* p = reinterpret_cast<const double2*>(mine);
@@ -1850,8 +1851,8 @@ __global__ __launch_bounds__(kWave * kLanesW) void k_path_scan_lanes(
         __syncthreads();  // the windows are read before the next ones are written
     }
     SGMM_STAMP(blockIdx.x, 3);
-    // 3. records (wave 0, lane v: episode e0 + v) and the generation tail
-    if (w == 0) {
+    // 3. records (the chain wave, lane v: episode e0 + v) and the generation tail
+    if (w == wc) {
         const int nv = min(kLanesW, n - e0);
         if (lane < nv) {
             const int ev = e0 + lane;
