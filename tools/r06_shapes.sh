@@ -16,5 +16,7 @@ run c6 -- --config 6 || exit 1
 run c4 -- --config 4 || exit 1
 run c4s4 -- --config 4 --shard-of 4 || exit 1
 run c5 -- --config 5 || exit 1
+run c5s2 -- --config 5 --shard-of 2 || exit 1
+run c5s4 -- --config 5 --shard-of 4 || exit 1
 run c5s8 -- --config 5 --shard-of 8 || exit 1
 run c5s16 -- --config 5 --shard-of 16 || exit 1
