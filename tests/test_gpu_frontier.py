@@ -338,3 +338,14 @@ def test_frontier_lanes_scan(sgmm, oracle, plan, lanes, groups):
     fit, trd, wf, wt = _run(sgmm, oracle, lens, 32, seed=71, sigma=0.5)
     assert np.array_equal(trd, wt)
     assert np.array_equal(fit, wf)
+
+
+@pytest.mark.parametrize("caps", [(3, -4), (1, -3), (0, 0)], ids=["8states", "offcentre", "1state"])
+def test_frontier_lanes_scan_inventory_ranges(sgmm, oracle, plan, caps):
+    """The lanes scan (k_path_scan_lanes<8> for 8 inventory states, <5> otherwise)
+    with caps other than +-2, NaN FPT bounds and fees, ragged lengths."""
+    plan(policy_path="frontier", groups=2, lanes_scan=1, fused_scan=0)
+    lens = 200 + (np.arange(23) * 211) % 2500
+    fit, trd, wf, wt = _run(sgmm, oracle, lens, 16, seed=73, caps=caps, sigma=0.6, nan_frac=0.03, fee=2e-5)
+    assert np.array_equal(trd, wt)
+    assert np.array_equal(fit, wf)
