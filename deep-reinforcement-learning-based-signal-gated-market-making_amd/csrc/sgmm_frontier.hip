@@ -125,8 +125,11 @@ __device__ __forceinline__ FusedChain fused_group(const FrontierArgs& args, int 
         }
         __syncthreads();
         if (w0 + kFusedWin < t1) gather(w0 + kFusedWin);
-        // every lane adds the window in order from LDS broadcast reads, 32 values
-        // per round trip (exact_sum_window's sequential chain)
+        // lane 0 adds the window in order from LDS, 32 values per round trip
+        // (exact_sum_window's sequential chain; on one lane rather than all 64 the
+        // walks sharing the SIMD lose less of the vector pipe: config 5's launch
+        // 1 270-1 285 -> 1 250-1 256 us, profiles/r06_fused/NOTES.md)
+        if (lane == 0) {
         const double2* p = reinterpret_cast<const double2*>(win);
         int i = 0;
         const int nc = n & ~31;
@@ -141,6 +144,8 @@ __device__ __forceinline__ FusedChain fused_group(const FrontierArgs& args, int 
             }
         }
         for (; i < n; ++i) S += win[i];
+        }
+        S = __longlong_as_double((long long)readlane64((uint64_t)__double_as_longlong(S), 0));
         __syncthreads();  // the window is read before the next one is written
     }
     cs.S = S;
