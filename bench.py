@@ -231,12 +231,16 @@ def latest_pmc(path_arg, config):
         return None
 
 
-def latest_trace_window(config, kname):
+def latest_trace_window(config, kname, steps=None):
     """The committed rocprofv3 kernel-trace measurement of the policy kernel over
     the same command's timed window (profiles/rNN_kernel_window_cC.txt, written by
-    tools/kt_window.py from `rocprofv3 --kernel-trace` of `bench.py --config C`)."""
+    tools/kt_window.py from `rocprofv3 --kernel-trace` of `bench.py --config C
+    --steps 20`; profiles/rNN_kernel_window_cC_sK.txt for K timed generations, e.g.
+    the no-flag command's 100, preferred when it matches)."""
     import re
-    cands = sorted((ROOT / "profiles").glob(f"r*_kernel_window_c{config}.txt"))
+    cands = sorted((ROOT / "profiles").glob(f"r*_kernel_window_c{config}_s{steps}.txt")) if steps else []
+    if not cands:
+        cands = sorted((ROOT / "profiles").glob(f"r*_kernel_window_c{config}.txt"))
     if not cands:
         return None
     fam = "k_policy_frontier" if kname == "policy_frontier" else "k_policy_table"
@@ -402,7 +406,7 @@ def main():
                                     "note": note},
                     "avg_launch_us": tab["avg_us"],
                     "launch_us_over_timed_window": _series(per_gen, kname, g0)}
-        tw = latest_trace_window(args.config, kname) if shard_of == 1 else None
+        tw = latest_trace_window(args.config, kname, args.steps) if shard_of == 1 else None
         if tw:
             # the same frac from the committed rocprof trace of this command (timed window)
             tw["frac"] = steps_per_launch * fl / (tw["us"] * 1e-6) / 1e12 / FP32_PEAK_TFLOPS
