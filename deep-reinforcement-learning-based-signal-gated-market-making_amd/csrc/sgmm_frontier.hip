@@ -31,8 +31,9 @@ __device__ unsigned int g_thwid[kStampWaves][2];  // HW_ID, XCC_ID of each wave
 // two groups (the launch plan's halves), group 0 sums its own chunks at once (its
 // path enters at inventory 0) and hands the chain on -- sum, state, trades, 16
 // bytes -- and group 1 continues over its own chunks: each wave reads only what it
-// wrote itself.  Only when group 1 finishes first does it hand its records and plane
-// rows over instead (re-stored write-through), for group 0 to continue with.  The
+// wrote itself.  Only when group 1 finishes before group 0 has handed the chain on
+// does it hand its records and plane rows over instead (re-stored write-through), for
+// group 0 to continue with.  The
 // chain's last wave adds the idle penalty (drl_engine.py:64-65), stores the record,
 // and the last record of a population runs the generation tail (tell_wave, the
 // argmax of StepArgs mode 3; mode 1's master regeneration would take the walk
