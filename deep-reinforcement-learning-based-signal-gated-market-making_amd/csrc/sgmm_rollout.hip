@@ -1710,17 +1710,16 @@ __global__ __launch_bounds__(TPB) void k_path_scan(
 #ifndef SGMM_LANES_W
 #define SGMM_LANES_W 4
 #endif
-constexpr int kLanesW = SGMM_LANES_W;       // episodes per workgroup
+constexpr int kLanesW = SGMM_LANES_W;       // episodes per workgroup (lanes_w picks 2 or 4 per launch)
 #ifndef SGMM_LANES_WIN
 #define SGMM_LANES_WIN 512
 #endif
 constexpr int kLanesWin = SGMM_LANES_WIN;   // ticks per window
 constexpr int kLanesPitch = kLanesWin + 2;  // doubles per LDS row (16-byte bank offset per row)
-static size_t lanes_scan_lds(int ngrp) {
-    return (size_t)kLanesW * kLanesPitch * sizeof(double) +
-           (size_t)kLanesW * kFrontierLanes * ngrp * (sizeof(uint32_t) + 1) + 64;
+static size_t lanes_scan_lds(int ngrp, int w) {
+    return (size_t)w * kLanesPitch * sizeof(double) + (size_t)w * kFrontierLanes * ngrp * (sizeof(uint32_t) + 1) + 64;
 }
-template <int NSM>
+template <int NSM, int kLanesW>
 __global__ __launch_bounds__(kWave * kLanesW) void k_path_scan_lanes(
     EpArrays ep, const sgmm_env_params* __restrict__ params, int32_t inv_min, const uint64_t* __restrict__ cmaps,
     const uint32_t* __restrict__ ctr32, const uint32_t* __restrict__ kinfo, const double* __restrict__ rew,
@@ -2646,9 +2645,18 @@ __global__ __launch_bounds__(1024) void k_zero_u32(uint32_t* __restrict__ p, int
 static bool lanes_scan(int nt, bool seq, const StepArgs& step, int32_t pop_eps) {
     const int v = plan_value(SGMM_PLAN_LANES_SCAN);
     if (v == 0 || !seq || (step.st && step.mode != 3)) return false;
-    if (step.st && step.pop_eps > 0 && step.pop_eps % kLanesW != 0) return false;
+    if (step.st && step.pop_eps > 0 && step.pop_eps % 4 != 0) return false;
     (void)pop_eps;
-    return v == 1 || nt == kWave;
+    return v > 0 || nt == kWave;
+}
+// episodes per lanes-scan workgroup: 2 from 2 048 episodes, 4 below (config 3 / 2 560
+// episodes: scan 53.5 against 55.5 us; config 5's 1-of-8 shard / 1 024: 31.1 against
+// 33.5 us with 2, profiles/r06_lanes/); SGMM_PLAN_LANES_SCAN = 2 or 4 forces it
+static int lanes_w(int32_t n, const StepArgs& step) {
+    const int v = plan_value(SGMM_PLAN_LANES_SCAN);
+    if (v == 2 || v == 4) return v;
+    (void)step;
+    return n >= 2048 ? 2 : kLanesW;
 }
 
 // the launches the feedback applies to: a mixed whole / halves plan of one wave
@@ -2813,14 +2821,20 @@ static int rollout_impl(const sgmm_ticks* ticks, const sgmm_episodes* eps,
         const int nt = scan_threads(eps->n);
         ep.seq_sum = scan_seq_sum(nt, false, vt) ? 1 : 0;
         if (fr && lanes_scan(nt, ep.seq_sum != 0, step, src.pop_eps)) {
-            const size_t lds = lanes_scan_lds(ep.ngrp);
-            const dim3 grid((eps->n + kLanesW - 1) / kLanesW), block(kWave * kLanesW);
-            if (nsi <= 5)
-                SGMM_LAUNCH(k_path_scan_lanes<5>, grid, block, lds, s, ep, params, eps->inv_min, cmaps,
-                            reinterpret_cast<const uint32_t*>(ctr), kinfo, rew, fitness, trades, step, eps->n);
-            else
-                SGMM_LAUNCH(k_path_scan_lanes<8>, grid, block, lds, s, ep, params, eps->inv_min, cmaps,
-                            reinterpret_cast<const uint32_t*>(ctr), kinfo, rew, fitness, trades, step, eps->n);
+            const int lw = lanes_w(eps->n, step);
+            const size_t lds = lanes_scan_lds(ep.ngrp, lw);
+            const dim3 grid((eps->n + lw - 1) / lw), block(kWave * lw);
+#define SGMM_LANES_LAUNCH(N_, W_)                                                                                 \
+    SGMM_LAUNCH((k_path_scan_lanes<N_, W_>), grid, block, lds, s, ep, params, eps->inv_min, cmaps,                \
+                reinterpret_cast<const uint32_t*>(ctr), kinfo, rew, fitness, trades, step, eps->n)
+            if (nsi <= 5) {
+                if (lw == 2) SGMM_LANES_LAUNCH(5, 2);
+                else SGMM_LANES_LAUNCH(5, 4);
+            } else {
+                if (lw == 2) SGMM_LANES_LAUNCH(8, 2);
+                else SGMM_LANES_LAUNCH(8, 4);
+            }
+#undef SGMM_LANES_LAUNCH
         } else if (size_t lds = (size_t)(nt == kWave ? 4 * kWave : nt) * kSumTpt * sizeof(double) +  // the window
                                 (fr ? (size_t)5 * kFrontierLanes * ep.ngrp : 0);  // chunk start states + merge info
                    fr) {

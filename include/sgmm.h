@@ -495,7 +495,8 @@ enum {
     SGMM_PLAN_SPILL = 9,         /* frontier spill deadline, us after a walk's start (0: off) */
     SGMM_PLAN_SEQ_SUM = 10,      /* path-scan episode sums: 0 exact parallel method, 1 sequential chain */
     SGMM_PLAN_FUSED_SCAN = 11,   /* frontier launches: 0 separate path scan, 1 scans fused into the walks */
-    SGMM_PLAN_LANES_SCAN = 12,   /* frontier path scan: 1 = 4 episodes per workgroup, chains in lanes; 0 = one per wave */
+    SGMM_PLAN_LANES_SCAN = 12,   /* frontier path scan: 1 = 2-4 episodes per workgroup, chains in lanes (2 / 4 force
+                                    the count); 0 = one episode per wave */
     SGMM_PLAN_N = 13
 };
 int sgmm_plan_set(int32_t knob, int32_t value);

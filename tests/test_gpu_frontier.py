@@ -325,13 +325,13 @@ def test_frontier_fused_scan_handoff_both_ways(sgmm, oracle, plan, seed):
     assert np.array_equal(fit, wf)
 
 
-@pytest.mark.parametrize("lanes", [0, 1], ids=["one_wave_scan", "lanes_scan"])
+@pytest.mark.parametrize("lanes", [0, 2, 4], ids=["one_wave_scan", "lanes_scan_w2", "lanes_scan_w4"])
 @pytest.mark.parametrize("groups", [1, 2, 4, 16], ids=["whole", "halves", "quarters", "16groups"])
 def test_frontier_lanes_scan(sgmm, oracle, plan, lanes, groups):
-    """The frontier path scan with 4 episodes per workgroup, their sequential chains
+    """The frontier path scan with 2 or 4 episodes per workgroup, their sequential chains
     in the lanes of one wave (k_path_scan_lanes), against the one-wave scan and the
     oracle: ragged lengths (the shorter episodes' windows padded with -0.0), empty
-    and one-tick episodes, a batch that is not a multiple of 4, 1-16 chunk groups."""
+    and one-tick episodes, a batch that is not a multiple of 2 or 4, 1-16 chunk groups."""
     plan(policy_path="frontier", groups=groups, lanes_scan=lanes, fused_scan=0)
     lens = [0, 1, 5, 64, 257, 511, 512, 513, 4560, 0, 9001, 3600, 700, 2, 1023, 1024, 1025, 4096, 100, 7,
             300, 301, 302, 2049, 17, 4561, 0, 33, 8191, 250, 251, 3001, 999, 1000, 1001, 64, 65]
